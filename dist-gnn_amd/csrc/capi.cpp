@@ -1,0 +1,366 @@
+// capi.cpp -- extern "C" boundary (include/dgs_amd.h).  Every entry point maps C++
+// exceptions to a -1 return + thread-local message.
+#include "../../include/dgs_amd.h"
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "services.h"
+
+using namespace dgs;
+
+namespace {
+thread_local std::string g_err;
+
+template <typename F>
+int guard(F &&f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception &e) {
+    g_err = e.what();
+  } catch (...) {
+    g_err = "unknown error";
+  }
+  return -1;
+}
+
+hipStream_t S(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Pointer usable by kernels: device memory or registered/pinned host memory.
+template <typename T>
+T *dev_ptr(T *p, const char *what) {
+  if (!p) return p;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, (const void *)p) != hipSuccess) {
+    (void)hipGetLastError();
+    throw Error(std::string(what) + " must be a device (CUDA) tensor or pinned host memory");
+  }
+  if (a.type == hipMemoryTypeHost) {
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, (void *)p, 0) == hipSuccess && d) return (T *)d;
+    (void)hipGetLastError();
+    return a.devicePointer ? (T *)a.devicePointer : p;
+  }
+  if (a.type == hipMemoryTypeUnregistered)
+    throw Error(std::string(what) + " must be a device (CUDA) tensor or pinned host memory");
+  return p;
+}
+
+HopScratch &op_scratch() {
+  static HopScratch ws;
+  return ws;
+}
+}  // namespace
+
+struct dgs_p2p_server {
+  P2PServer *s;
+};
+struct dgs_sampler {
+  Sampler *s;
+};
+struct dgs_feature_server {
+  FeatureServer *s;
+};
+
+extern "C" {
+
+const char *dgs_last_error(void) { return g_err.c_str(); }
+
+const char *dgs_version(void) { return "dgs_amd 0.1 (gfx950, wave64, HIP)"; }
+
+// ------------------------------------------------------------------ context
+int dgs_get_unique_id(int64_t *out_id16) {
+  return guard([&] {
+    static_assert(sizeof(ncclUniqueId) <= 16 * sizeof(int64_t), "unique id size");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) throw Error(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    std::memset(out_id16, 0, 16 * sizeof(int64_t));
+    std::memcpy(out_id16, &id, sizeof(id));
+  });
+}
+
+int dgs_set_nccl(int64_t nranks, const int64_t *unique_id, int64_t n_id, int64_t rank) {
+  return guard([&] {
+    DGS_CHECK(n_id * (int64_t)sizeof(int64_t) >= (int64_t)sizeof(ncclUniqueId),
+              "unique id array too short");
+    Comm::get().init((int)nranks, unique_id, (int)rank);
+  });
+}
+
+int dgs_get_local_rank(void) { return Comm::get().rank(); }
+int dgs_get_world_size(void) { return Comm::get().world(); }
+
+int dgs_barrier(void) {
+  return guard([&] { Comm::get().barrier(); });
+}
+
+int dgs_allgather_sizes(int64_t my_size, int64_t *all_sizes) {
+  return guard([&] {
+    std::vector<int64_t> v = Comm::get().allgather_sizes(my_size);
+    std::memcpy(all_sizes, v.data(), sizeof(int64_t) * v.size());
+  });
+}
+
+int dgs_allgather_bytes(const void *send, int64_t send_bytes, void *const *recv,
+                        const int64_t *recv_bytes, void *stream) {
+  return guard([&] { Comm::get().allgather_bytes(send, send_bytes, recv, recv_bytes, S(stream)); });
+}
+
+uint64_t dgs_randn_uint64(void) { return rng().next(); }
+
+int dgs_set_random_seed(uint64_t seed) {
+  rng().set_seed(seed);
+  return 0;
+}
+
+// ------------------------------------------------------------------ host memory
+int dgs_host_register(void *ptr, int64_t bytes) {
+  return guard([&] {
+    if (!ptr || bytes <= 0) return;
+    DGS_HIP(hipHostRegister(ptr, (size_t)bytes, hipHostRegisterMapped));
+  });
+}
+
+int dgs_host_unregister(void *ptr) {
+  return guard([&] {
+    if (!ptr) return;
+    DGS_HIP(hipHostUnregister(ptr));
+  });
+}
+
+// ------------------------------------------------------------------ ops
+int dgs_index_select(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
+                     int64_t n, void *out, void *stream) {
+  return guard([&] {
+    gather_plain(dev_ptr(data, "data"), row_bytes, dev_ptr(nid, "nid"), nid_bytes, n, out,
+                 S(stream));
+  });
+}
+
+int dgs_sample_neighbors(const int64_t *seeds, int64_t Sn, const int64_t *indptr,
+                         const int64_t *indices, const float *probs, int64_t num_picks,
+                         int replace, int64_t *out_row, int64_t *out_col, int64_t *nnz_out,
+                         void *stream) {
+  return guard([&] {
+    hipStream_t st = S(stream);
+    RowSrc src{};
+    src.ntab = nullptr;
+    src.indptr = dev_ptr(indptr, "indptr");
+    src.indices.p[0] = dev_ptr(indices, "indices");
+    src.probs.p[0] = dev_ptr(probs, "probs");
+    seeds = dev_ptr(seeds, "seeds");
+    HopScratch &ws = op_scratch();
+    int64_t *tmp = nullptr;  // [0] = nnz, then rowpos[S*k]
+    const int64_t cap = Sn * num_picks;
+    DGS_HIP(hipMallocAsync((void **)&tmp, sizeof(int64_t) * (size_t)(cap + 1), st));
+    sample_hop(src, seeds, Sn, num_picks, replace != 0, probs != nullptr, rng().next(), tmp + 1,
+               out_col, tmp, ws, st);
+    int64_t nnz = 0;
+    DGS_HIP(hipMemcpyAsync(&nnz, tmp, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    DGS_HIP(hipStreamSynchronize(st));
+    take_i64(seeds, tmp + 1, nnz, out_row, st);
+    DGS_HIP(hipFreeAsync(tmp, st));
+    *nnz_out = nnz;
+  });
+}
+
+int dgs_relabel(const int64_t *const *maps, const int64_t *map_sizes, int n_maps,
+                const int64_t *const *reqs, const int64_t *req_sizes, int n_reqs,
+                int64_t *unique_out, int64_t *n_unique, int64_t *const *req_out, void *stream) {
+  return guard([&] {
+    hipStream_t st = S(stream);
+    int64_t nm = 0, nr = 0;
+    for (int i = 0; i < n_maps; ++i) nm += map_sizes[i];
+    for (int i = 0; i < n_reqs; ++i) nr += req_sizes[i];
+    int64_t *buf = nullptr;  // mapping[nm] | req[nr] | req_out[nr] | count
+    DGS_HIP(hipMallocAsync((void **)&buf, sizeof(int64_t) * (size_t)(nm + 2 * nr + 1), st));
+    int64_t off = 0;
+    for (int i = 0; i < n_maps; ++i) {
+      if (map_sizes[i] > 0)
+        DGS_HIP(hipMemcpyAsync(buf + off, dev_ptr(maps[i], "mapping tensor"),
+                               sizeof(int64_t) * map_sizes[i], hipMemcpyDefault, st));
+      off += map_sizes[i];
+    }
+    for (int i = 0; i < n_reqs; ++i) {
+      if (req_sizes[i] > 0)
+        DGS_HIP(hipMemcpyAsync(buf + off, dev_ptr(reqs[i], "relabel tensor"),
+                               sizeof(int64_t) * req_sizes[i], hipMemcpyDefault, st));
+      off += req_sizes[i];
+    }
+    int64_t *d_cnt = buf + nm + 2 * nr;
+    relabel_generic(buf, nm, buf + nm, nr, unique_out, buf + nm + nr, d_cnt, op_scratch(), st);
+    off = nm + nr;
+    for (int i = 0; i < n_reqs; ++i) {
+      if (req_sizes[i] > 0)
+        DGS_HIP(hipMemcpyAsync(req_out[i], buf + off, sizeof(int64_t) * req_sizes[i],
+                               hipMemcpyDeviceToDevice, st));
+      off += req_sizes[i];
+    }
+    int64_t u = 0;
+    DGS_HIP(hipMemcpyAsync(&u, d_cnt, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    DGS_HIP(hipStreamSynchronize(st));
+    DGS_HIP(hipFreeAsync(buf, st));
+    *n_unique = u;
+  });
+}
+
+int dgs_extract_indptr(const int64_t *nids, int64_t n, const int64_t *indptr,
+                       int64_t *sub_indptr, void *stream) {
+  return guard([&] {
+    extract_indptr(dev_ptr(nids, "nids"), n, dev_ptr(indptr, "indptr"), sub_indptr, S(stream));
+  });
+}
+
+int dgs_extract_edge_data(const int64_t *nids, int64_t n, const int64_t *indptr,
+                          const int64_t *sub_indptr, const void *edge_data, int64_t elem_bytes,
+                          void *sub_edge_data, void *stream) {
+  return guard([&] {
+    extract_edge_data(dev_ptr(nids, "nids"), n, dev_ptr(indptr, "indptr"),
+                      dev_ptr(sub_indptr, "sub_indptr"), dev_ptr(edge_data, "edge_data"),
+                      elem_bytes, sub_edge_data, S(stream));
+  });
+}
+
+int dgs_compute_frontier_heat(const int64_t *seeds, int64_t n_seeds, const int64_t *indptr,
+                              const int64_t *indices, const float *probs,
+                              const float *seeds_heat, int64_t num_nodes, int64_t num_picks,
+                              int64_t indptr_diff, float *frontier_heat, void *stream) {
+  return guard([&] {
+    hipStream_t st = S(stream);
+    DGS_HIP(hipMemsetAsync(frontier_heat, 0, sizeof(float) * (size_t)num_nodes, st));
+    heat(dev_ptr(seeds, "seeds"), n_seeds, dev_ptr(indptr, "indptr"),
+         dev_ptr(indices, "indices"), dev_ptr(probs, "probs"), dev_ptr(seeds_heat, "seeds_heat"),
+         num_picks, indptr_diff, frontier_heat, st);
+  });
+}
+
+// ------------------------------------------------------------------ TensorP2PServer
+int dgs_p2p_server_create(const void *src, int64_t items, int64_t item_bytes,
+                          dgs_p2p_server **out) {
+  return guard([&] { *out = new dgs_p2p_server{new P2PServer(src, items, item_bytes)}; });
+}
+
+int dgs_p2p_server_device_ptr(dgs_p2p_server *s, int64_t rank, void **ptr, int64_t *items) {
+  return guard([&] {
+    DGS_CHECK(rank >= 0 && rank < s->s->world(), "rank out of range");
+    *ptr = s->s->ptr((int)rank);
+    *items = s->s->items((int)rank);
+  });
+}
+
+int dgs_p2p_server_destroy(dgs_p2p_server *s) {
+  return guard([&] {
+    delete s->s;
+    delete s;
+  });
+}
+
+// ------------------------------------------------------------------ sampler
+int dgs_sampler_create(const int64_t *indptr, const int64_t *indices, const float *probs,
+                       int64_t num_nodes, int64_t num_edges, const int64_t *cache_nids,
+                       int64_t n_cache, int64_t device_id, dgs_sampler **out) {
+  return guard([&] {
+    *out = new dgs_sampler{
+        new Sampler(indptr, indices, probs, num_nodes, num_edges, cache_nids, n_cache, device_id)};
+  });
+}
+
+int dgs_sampler_bounds(const dgs_sampler *s, int64_t n_seeds, const int64_t *fan_out, int L,
+                       int64_t *frontier_cap, int64_t *edge_cap) {
+  return guard([&] { s->s->bounds(n_seeds, fan_out, L, frontier_cap, edge_cap); });
+}
+
+int dgs_sampler_sample(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
+                       const int64_t *fan_out, int L, int replace, int64_t *const *frontiers,
+                       int64_t *const *rows, int64_t *const *cols, int64_t *sizes_out,
+                       void *stream) {
+  return guard([&] {
+    s->s->sample(dev_ptr(seeds, "seeds"), n_seeds, fan_out, L, replace != 0, frontiers, rows,
+                 cols, sizes_out, S(stream));
+  });
+}
+
+int dgs_sampler_local_cache(const dgs_sampler *s, const int64_t **sub_indptr, int64_t *n_rows,
+                            const int64_t **sub_indices, int64_t *n_edges,
+                            const float **sub_probs) {
+  return guard([&] {
+    *sub_indptr = s->s->sub_indptr();
+    *n_rows = s->s->n_rows();
+    *sub_indices = s->s->sub_indices();
+    *n_edges = s->s->n_edges();
+    *sub_probs = s->s->sub_probs();
+  });
+}
+
+int dgs_sampler_cache_map_size(const dgs_sampler *s, int64_t *n) {
+  return guard([&] { *n = s->s->cache_map_size(); });
+}
+
+int dgs_sampler_cache_map_fill(const dgs_sampler *s, int64_t *key, int64_t *idx,
+                               int64_t *devid, void *stream) {
+  return guard([&] { s->s->cache_map_fill(key, idx, devid, S(stream)); });
+}
+
+int dgs_sampler_destroy(dgs_sampler *s) {
+  return guard([&] {
+    delete s->s;
+    delete s;
+  });
+}
+
+// ------------------------------------------------------------------ feature server
+int dgs_feature_server_create(const void *data, int64_t num_rows, int64_t row_bytes,
+                              const int64_t *cache_nids, int64_t n_cache, int64_t device_id,
+                              dgs_feature_server **out) {
+  return guard([&] {
+    *out = new dgs_feature_server{
+        new FeatureServer(data, num_rows, row_bytes, cache_nids, n_cache, device_id)};
+  });
+}
+
+int dgs_feature_server_gather(dgs_feature_server *s, const int64_t *nids, int64_t n, void *out,
+                              void *stream) {
+  return guard([&] { s->s->gather(dev_ptr(nids, "nids"), n, out, S(stream)); });
+}
+
+int dgs_feature_server_local_cache(const dgs_feature_server *s, const void **ptr,
+                                   int64_t *rows) {
+  return guard([&] {
+    *ptr = s->s->local();
+    *rows = s->s->local_rows();
+  });
+}
+
+int dgs_feature_server_destroy(dgs_feature_server *s) {
+  return guard([&] {
+    delete s->s;
+    delete s;
+  });
+}
+
+// ------------------------------------------------------------------ profiling
+int dgs_profile_enable(int on) {
+  return guard([&] {
+    profile_collect();
+    profiler().on = on != 0;
+  });
+}
+
+int dgs_profile_read(double *gather_ms, int64_t *gather_launches, double *sample_ms,
+                     int64_t *sample_calls) {
+  return guard([&] {
+    profile_collect();
+    Profiler &p = profiler();
+    *gather_ms = p.gather_ms;
+    *gather_launches = p.gather_n;
+    *sample_ms = p.sample_ms;
+    *sample_calls = p.sample_n;
+    p.gather_ms = p.sample_ms = 0;
+    p.gather_n = p.sample_n = 0;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,197 @@
+// context.cpp -- launch-seed RNG, RCCL communicator, pointer utilities, profiler.
+#include "context.h"
+
+#include <cstring>
+
+#include "dgs_ops.h"
+
+namespace dgs {
+
+RandomEngine &rng() {
+  static RandomEngine e;
+  return e;
+}
+
+// ------------------------------------------------------------------ communicator
+#define DGS_NCCL(call)                                                                  \
+  do {                                                                                  \
+    ncclResult_t r_ = (call);                                                           \
+    if (r_ != ncclSuccess)                                                              \
+      throw ::dgs::Error(std::string(#call) + " failed: " + ncclGetErrorString(r_));    \
+  } while (0)
+
+Comm &Comm::get() {
+  static Comm c;
+  return c;
+}
+
+void Comm::init(int nranks, const void *unique_id, int rank) {
+  DGS_CHECK(comm_ == nullptr, "communicator already initialised");
+  DGS_CHECK(nranks >= 1 && nranks <= kMaxDevices, "world size must be 1..8 (one node)");
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id, sizeof(id));
+  DGS_NCCL(ncclCommInitRank(&comm_, nranks, id, rank));
+  DGS_NCCL(ncclCommUserRank(comm_, &rank_));
+  DGS_NCCL(ncclCommCount(comm_, &world_));
+  DGS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  DGS_HIP(hipMalloc(&dbuf_, sizeof(float)));
+  DGS_HIP(hipMalloc(&dsizes_, sizeof(int64_t) * (kMaxDevices + 1)));
+}
+
+void Comm::barrier() {
+  if (!comm_) return;
+  DGS_NCCL(ncclAllReduce(dbuf_, dbuf_, 1, ncclFloat, ncclSum, comm_, stream_));
+  DGS_HIP(hipStreamSynchronize(stream_));
+}
+
+std::vector<int64_t> Comm::allgather_sizes(int64_t mine) {
+  std::vector<int64_t> out(world_, mine);
+  if (!comm_ || world_ == 1) return out;
+  // device staging (the reference hands a host-registered vector to NCCL,
+  // nccl_context.cc:61-77; RCCL gets device buffers here)
+  DGS_HIP(hipMemcpyAsync(dsizes_ + kMaxDevices, &mine, sizeof(int64_t), hipMemcpyHostToDevice,
+                         stream_));
+  DGS_NCCL(ncclAllGather(dsizes_ + kMaxDevices, dsizes_, 1, ncclInt64, comm_, stream_));
+  DGS_HIP(hipMemcpyAsync(out.data(), dsizes_, sizeof(int64_t) * world_, hipMemcpyDeviceToHost,
+                         stream_));
+  DGS_HIP(hipStreamSynchronize(stream_));
+  return out;
+}
+
+void Comm::allgather_bytes(const void *send, int64_t send_bytes, void *const *recv,
+                           const int64_t *recv_bytes, hipStream_t st) {
+  if (recv[rank_] != send && send_bytes > 0)
+    DGS_HIP(hipMemcpyAsync(recv[rank_], send, send_bytes, hipMemcpyDeviceToDevice, st));
+  if (!comm_ || world_ == 1) return;
+  DGS_HIP(hipStreamSynchronize(st));
+  DGS_NCCL(ncclGroupStart());
+  for (int i = 0; i < world_; ++i) {
+    if (i == rank_) continue;
+    DGS_NCCL(ncclSend(send, (size_t)send_bytes, ncclChar, i, comm_, stream_));
+    DGS_NCCL(ncclRecv(recv[i], (size_t)recv_bytes[i], ncclChar, i, comm_, stream_));
+  }
+  DGS_NCCL(ncclGroupEnd());
+  DGS_HIP(hipStreamSynchronize(stream_));
+}
+
+std::vector<void *> Comm::allgather_device(const void *send, int64_t send_bytes,
+                                           std::vector<int64_t> *bytes_out) {
+  std::vector<int64_t> sizes = allgather_sizes(send_bytes);
+  std::vector<void *> bufs(world_, nullptr);
+  for (int i = 0; i < world_; ++i) DGS_HIP(hipMalloc(&bufs[i], sizes[i] > 0 ? sizes[i] : 1));
+  allgather_bytes(send, send_bytes, bufs.data(), sizes.data(), stream_);
+  DGS_HIP(hipStreamSynchronize(stream_));
+  if (bytes_out) *bytes_out = sizes;
+  return bufs;
+}
+
+// ------------------------------------------------------------------ pointers
+bool is_device_pointer(const void *p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
+         a.type == hipMemoryTypeUnified;
+}
+
+void *device_view(const void *p, int64_t bytes, bool *registered_here) {
+  if (registered_here) *registered_here = false;
+  if (!p) return nullptr;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) == hipSuccess) {
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
+        a.type == hipMemoryTypeUnified)
+      return const_cast<void *>(p);
+    if (a.type == hipMemoryTypeHost) {
+      void *d = nullptr;
+      if (hipHostGetDevicePointer(&d, const_cast<void *>(p), 0) == hipSuccess && d) return d;
+      (void)hipGetLastError();
+      return a.devicePointer ? a.devicePointer : const_cast<void *>(p);
+    }
+  } else {
+    (void)hipGetLastError();
+  }
+  // pageable host memory: register it (mapped) for zero-copy device reads
+  DGS_HIP(hipHostRegister(const_cast<void *>(p), (size_t)(bytes > 0 ? bytes : 1),
+                          hipHostRegisterMapped));
+  if (registered_here) *registered_here = true;
+  void *d = nullptr;
+  DGS_HIP(hipHostGetDevicePointer(&d, const_cast<void *>(p), 0));
+  return d;
+}
+
+// ------------------------------------------------------------------ profiler
+namespace {
+struct EvPair {
+  hipEvent_t a, b;
+  int which;
+};
+std::vector<EvPair> &pending() {
+  static std::vector<EvPair> v;
+  return v;
+}
+std::vector<hipEvent_t> &pool() {
+  static std::vector<hipEvent_t> v;
+  return v;
+}
+hipEvent_t take_event() {
+  auto &p = pool();
+  if (!p.empty()) {
+    hipEvent_t e = p.back();
+    p.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  DGS_HIP(hipEventCreate(&e));
+  return e;
+}
+}  // namespace
+
+Profiler &profiler() {
+  static Profiler p;
+  return p;
+}
+
+void profile_begin(hipStream_t st, int which) {
+  if (!profiler().on) return;
+  EvPair ev{take_event(), nullptr, which};
+  DGS_HIP(hipEventRecord(ev.a, st));
+  pending().push_back(ev);
+}
+
+void profile_end(hipStream_t st, int which) {
+  if (!profiler().on) return;
+  auto &pv = pending();
+  for (auto it = pv.rbegin(); it != pv.rend(); ++it) {
+    if (it->which == which && it->b == nullptr) {
+      it->b = take_event();
+      DGS_HIP(hipEventRecord(it->b, st));
+      return;
+    }
+  }
+}
+
+void profile_collect() {
+  auto &pv = pending();
+  for (auto &ev : pv) {
+    if (!ev.b) continue;
+    DGS_HIP(hipEventSynchronize(ev.b));
+    float ms = 0;
+    DGS_HIP(hipEventElapsedTime(&ms, ev.a, ev.b));
+    if (ev.which == 0) {
+      profiler().gather_ms += ms;
+      profiler().gather_n += 1;
+    } else {
+      profiler().sample_ms += ms;
+      profiler().sample_n += 1;
+    }
+    pool().push_back(ev.a);
+    pool().push_back(ev.b);
+  }
+  pv.clear();
+}
+
+}  // namespace dgs

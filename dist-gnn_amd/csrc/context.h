@@ -1,0 +1,72 @@
+// context.h -- process-global context: launch-seed RNG, RCCL communicator, host-memory
+// registration and the kernel profiler.
+//
+// Reference: src/context/context.{h,cc} (RandomEngine, randn_uint64),
+// src/nccl/nccl_context.{h,cc} (NCCLContext singleton), src/common/pin_memory.cc.
+#pragma once
+
+#include <rccl/rccl.h>
+
+#include <mutex>
+#include <random>
+#include <vector>
+
+#include "dgs_common.h"
+
+namespace dgs {
+
+// std::mt19937_64 + full-range uniform_int_distribution == raw engine output (libstdc++),
+// seeded from std::random_device like the reference; set_seed() makes runs reproducible.
+class RandomEngine {
+ public:
+  RandomEngine() : gen_(std::random_device()()) {}
+  uint64_t next() {
+    std::lock_guard<std::mutex> g(mu_);
+    return dis_(gen_);
+  }
+  void set_seed(uint64_t s) {
+    std::lock_guard<std::mutex> g(mu_);
+    gen_.seed(s);
+    dis_.reset();
+  }
+
+ private:
+  std::mutex mu_;
+  std::mt19937_64 gen_;
+  std::uniform_int_distribution<uint64_t> dis_{0, 0xFFFFFFFFFFFFFFFFULL};
+};
+RandomEngine &rng();
+
+// RCCL communicator for the setup collectives (no collective runs in the sampling /
+// gather hot loop: remote rows are read one-sided through IPC-mapped peer memory).
+class Comm {
+ public:
+  static Comm &get();
+  void init(int nranks, const void *unique_id, int rank);
+  bool initialized() const { return comm_ != nullptr; }
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  void barrier();
+  std::vector<int64_t> allgather_sizes(int64_t mine);
+  // grouped ncclSend/ncclRecv of byte payloads (recv[rank_] may alias send)
+  void allgather_bytes(const void *send, int64_t send_bytes, void *const *recv,
+                       const int64_t *recv_bytes, hipStream_t st);
+  // convenience: all-gather a device byte buffer into freshly allocated device buffers
+  std::vector<void *> allgather_device(const void *send, int64_t send_bytes,
+                                       std::vector<int64_t> *bytes_out);
+
+ private:
+  ncclComm_t comm_ = nullptr;
+  int rank_ = 0, world_ = 1;
+  hipStream_t stream_ = nullptr;
+  float *dbuf_ = nullptr;
+  int64_t *dsizes_ = nullptr;
+};
+
+// Device-accessible pointer for `p`: device memory is returned as is; pinned / registered
+// host memory is translated; pageable host memory is registered (mapped) first and
+// *registered_here is set so the owner can unregister it.
+void *device_view(const void *p, int64_t bytes, bool *registered_here);
+bool is_device_pointer(const void *p);
+
+}  // namespace dgs

@@ -1,0 +1,137 @@
+// dgs_common.h -- shared host/device utilities for the DGS-AMD HIP library (gfx950).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace dgs {
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define DGS_HIP(call)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (call);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      throw ::dgs::Error(std::string(#call) + " failed: " + hipGetErrorString(e_) +     \
+                         " (" + __FILE__ + ":" + std::to_string(__LINE__) + ")");       \
+  } while (0)
+
+#define DGS_CHECK(cond, msg)                                                            \
+  do {                                                                                  \
+    if (!(cond)) throw ::dgs::Error(std::string("DGS check failed: ") + (msg));         \
+  } while (0)
+
+// Launch-error check after a kernel launch (no sync).
+#define DGS_LAUNCH_CHECK() DGS_HIP(hipGetLastError())
+
+constexpr int kWave = 64;
+
+// Grow-only device scratch buffer owned by a service object.
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  // Returns true when (re)allocated (contents undefined).
+  bool ensure(size_t need) {
+    if (need <= bytes && p) return false;
+    release();
+    size_t n = need < 256 ? 256 : need;
+    DGS_HIP(hipMalloc(&p, n));
+    bytes = n;
+    return true;
+  }
+  template <typename T>
+  T *as() const {
+    return reinterpret_cast<T *>(p);
+  }
+};
+
+// Pinned host staging for small D2H size reads.
+struct HostPinned {
+  void *p = nullptr;
+  size_t bytes = 0;
+  ~HostPinned() {
+    if (p) (void)hipHostFree(p);
+  }
+  void ensure(size_t need) {
+    if (need <= bytes && p) return;
+    if (p) (void)hipHostFree(p);
+    DGS_HIP(hipHostMalloc(&p, need, hipHostMallocDefault));
+    bytes = need;
+  }
+  template <typename T>
+  T *as() const {
+    return reinterpret_cast<T *>(p);
+  }
+};
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline uint64_t next_pow2(uint64_t x) {
+  uint64_t c = 1;
+  while (c < x) c <<= 1;
+  return c;
+}
+
+// ---------------------------------------------------------------------------------
+// Node-location encoding used by the graph shard context and the feature table.
+// A location is 0..kMaxDevices-1 (a GPU rank of the communicator) or kLocHost.
+constexpr int kMaxDevices = 8;
+constexpr int kLocHost = kMaxDevices;  // index into pointer tables
+constexpr int kLocShift = 56;
+constexpr int64_t kOffMask = (int64_t(1) << kLocShift) - 1;
+
+// Per-location base pointers, passed by value in kernel arguments (no device-side
+// pointer table indirection).
+struct PtrTable {
+  const void *p[kMaxDevices + 1];
+};
+
+// Graph node table entry (16 B, one load per seed):
+//   off = offset of the node's first edge inside its location's edge arrays,
+//   dl  = degree | (location << 56).
+struct NodeEntry {
+  int64_t off;
+  int64_t dl;
+};
+
+// ---------------------------------------------------------------------------------
+// Device helpers
+#ifdef __HIPCC__
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k.x += 0x9E3779B9u;
+      k.y += 0xBB67AE85u;
+    }
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+  }
+  return c;
+}
+
+__device__ __forceinline__ uint32_t u4_get(const uint4 &v, int w) {
+  return w == 0 ? v.x : (w == 1 ? v.y : (w == 2 ? v.z : v.w));
+}
+
+// curand_uniform(): x * 2^-32 + 2^-33 (exact product, single rounding in the add).
+__device__ __forceinline__ float curand_uniform_from(uint32_t x) {
+  return __fadd_rn(__fmul_rn((float)x, 2.3283064365386963e-10f), 1.1641532182693481e-10f);
+}
+#endif
+
+}  // namespace dgs

@@ -1,0 +1,100 @@
+// dgs_ops.h -- host-side launchers of the DGS-AMD HIP kernels (internal C++ interface).
+#pragma once
+
+#include "dgs_common.h"
+
+namespace dgs {
+
+// ---------------------------------------------------------------- gather (gather.hip)
+// out[i, :] = data[nid[i], :], a row_bytes byte copy per row.
+void gather_plain(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
+                  int64_t n, void *out, hipStream_t st);
+// out[i, :] = row (ftab[nids[i]]) where ftab entries are (loc << 56) | row and loc indexes
+// `bases` (kLocHost = host array indexed by the nid itself).
+void gather_table(const int64_t *ftab, PtrTable bases, int64_t row_bytes, const int64_t *nids,
+                  int64_t n, void *out, hipStream_t st);
+// ftab[v] = (kLocHost << 56) | v for v < n
+void ftab_init_host(int64_t *ftab, int64_t n, hipStream_t st);
+// ftab[nids[i]] = (loc << 56) | i
+void ftab_assign(int64_t *ftab, const int64_t *nids, int64_t n, int loc, hipStream_t st);
+
+// ---------------------------------------------------------------- CSR utilities (csr.hip)
+// sub_indptr[i] = sum_{j<i} deg(nids[j]), i = 0..n
+void extract_indptr(const int64_t *nids, int64_t n, const int64_t *indptr, int64_t *sub_indptr,
+                    hipStream_t st);
+void extract_edge_data(const int64_t *nids, int64_t n, const int64_t *indptr,
+                       const int64_t *sub_indptr, const void *edge_data, int64_t elem_bytes,
+                       void *sub, hipStream_t st);
+// node table: ntab[v] = {indptr[v], deg(v) | host}
+void ntab_init_host(NodeEntry *ntab, const int64_t *indptr, int64_t n, hipStream_t st);
+// ntab[nids[i]] = {sub_indptr[i], (sub_indptr[i+1]-sub_indptr[i]) | loc<<56}
+void ntab_assign(NodeEntry *ntab, const int64_t *nids, const int64_t *sub_indptr, int64_t n,
+                 int loc, hipStream_t st);
+// Compacts a (loc << 56 | row) table into (nid, row, loc) triples for every node whose
+// location is a GPU; *d_count receives the count.  key/idx/devid may be null (count only).
+void cache_map_compact(const int64_t *tab, int64_t n, int64_t *key, int64_t *idx,
+                       int64_t *devid, int64_t *d_count, hipStream_t st);
+void heat(const int64_t *seeds, int64_t n_seeds, const int64_t *indptr, const int64_t *indices,
+          const float *probs, const float *seeds_heat, int64_t num_picks, int64_t indptr_diff,
+          float *frontier_heat, hipStream_t st);
+
+// ---------------------------------------------------------------- scan (scan.hip)
+// Single-workgroup exclusive scan of n int64 values in place into out[0..n], out[n] = total.
+void scan_small(const int64_t *in, int64_t n, int64_t *out, hipStream_t st);
+// Device-wide exclusive scan: out[0..n] (out[n] = total). scratch >= scan_scratch_bytes(n).
+size_t scan_scratch_bytes(int64_t n);
+void scan_exclusive(const int64_t *in, int64_t n, int64_t *out, void *scratch, hipStream_t st);
+
+// ---------------------------------------------------------------- sampling (sample.hip)
+struct RowSrc {
+  // Node lookup: either a node table (graph shard context) or a plain CSR indptr.
+  const NodeEntry *ntab;  // if non-null
+  const int64_t *indptr;  // else
+  PtrTable indices;       // per-location edge arrays (indices)
+  PtrTable probs;         // per-location probabilities (biased) or all null
+};
+
+struct HopScratch {
+  DevBuf rowinfo, bsum, boff, hub, hubslot, rowpos, slot_of, tkey, tval, tlab, misc, cdf;
+  HostPinned host;
+  uint64_t table_cap = 0;  // capacity currently allocated and clean
+  bool table_dirty = false;
+};
+
+// One sampling hop over `seeds[S]` (device):
+//   writes rowpos[e] (index of the seed row of edge e) and col[e] (neighbour nid),
+//   d_nnz receives nnz (device).  Capacities: S * k.
+void sample_hop(const RowSrc &src, const int64_t *seeds, int64_t S, int64_t k, bool replace,
+                bool bias, uint64_t launch_seed, int64_t *rowpos, int64_t *col, int64_t *d_nnz,
+                HopScratch &ws, hipStream_t st);
+
+// Relabel for the node-classification hop: mapping = cat(seeds[S], col[nnz]) where nnz is
+// read from d_nnz (device); writes unique ids to `unique` (first-occurrence order),
+// relabeled rows/cols to out_row/out_col (col may alias out_col), U to d_nunique.
+void relabel_hop(const int64_t *seeds, int64_t S, const int64_t *col, const int64_t *d_nnz,
+                 int64_t nnz_cap, const int64_t *rowpos, int64_t *unique, int64_t *out_row,
+                 int64_t *out_col, int64_t *d_nunique, HopScratch &ws, hipStream_t st);
+
+// Generic relabel (TensorRelabelCUDA): mapping[nm], req[nr] -> unique, relabeled req (-1 if
+// absent), d_nunique.
+void relabel_generic(const int64_t *mapping, int64_t nm, const int64_t *req, int64_t nr,
+                     int64_t *unique, int64_t *req_out, int64_t *d_nunique, HopScratch &ws,
+                     hipStream_t st);
+
+// gather rows of `seeds` by rowpos (coo_row of the standalone sampler op)
+void take_i64(const int64_t *src, const int64_t *idx, int64_t n, int64_t *out, hipStream_t st);
+
+// ---------------------------------------------------------------- profiling
+struct Profiler {
+  bool on = false;
+  double gather_ms = 0, sample_ms = 0;
+  int64_t gather_n = 0, sample_n = 0;
+};
+Profiler &profiler();
+// Records begin/end events around `fn` on `st` when profiling is on; the elapsed time is
+// collected lazily by profile_collect().
+void profile_begin(hipStream_t st, int which);
+void profile_end(hipStream_t st, int which);
+void profile_collect();
+
+}  // namespace dgs

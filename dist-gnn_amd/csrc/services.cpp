@@ -1,0 +1,285 @@
+// services.cpp -- TensorP2PServer, P2PCacheSampler, P2PCacheFeatureServer.
+#include "services.h"
+
+#include <cstring>
+
+namespace dgs {
+
+// ============================================================== P2PServer
+// tensor_p2p_cache.cc:11-118: raw device block, IPC handle all-gather, peer handles opened
+// with lazy peer access; the destructor closes them behind a collective barrier.
+P2PServer::P2PServer(const void *src, int64_t items, int64_t item_bytes) {
+  const int64_t bytes = items * item_bytes;
+  void *block = nullptr;
+  DGS_HIP(hipMalloc(&block, bytes > 0 ? bytes : 1));
+  if (bytes > 0) DGS_HIP(hipMemcpy(block, src, bytes, hipMemcpyDefault));
+  item_bytes_ = item_bytes;
+  Comm &c = Comm::get();
+  rank_ = c.rank();
+  world_ = c.world();
+  ptrs_.assign(world_, nullptr);
+  ptrs_[rank_] = block;
+  items_.assign(world_, items);
+  share();
+}
+
+P2PServer *P2PServer::adopt(void *block, int64_t items, int64_t item_bytes) {
+  P2PServer *s = new P2PServer();
+  s->item_bytes_ = item_bytes;
+  Comm &c = Comm::get();
+  s->rank_ = c.rank();
+  s->world_ = c.world();
+  s->ptrs_.assign(s->world_, nullptr);
+  s->ptrs_[s->rank_] = block;
+  s->items_.assign(s->world_, items);
+  s->share();
+  return s;
+}
+
+void P2PServer::share() {
+  Comm &c = Comm::get();
+  if (world_ <= 1) return;
+  items_ = c.allgather_sizes(items_[rank_]);
+  hipIpcMemHandle_t h;
+  DGS_HIP(hipIpcGetMemHandle(&h, ptrs_[rank_]));
+  void *dh = nullptr;
+  DGS_HIP(hipMalloc(&dh, sizeof(h)));
+  DGS_HIP(hipMemcpy(dh, &h, sizeof(h), hipMemcpyHostToDevice));
+  std::vector<int64_t> nbytes;
+  std::vector<void *> all = c.allgather_device(dh, sizeof(h), &nbytes);
+  DGS_HIP(hipFree(dh));
+  c.barrier();
+  for (int i = 0; i < world_; ++i) {
+    hipIpcMemHandle_t hi;
+    DGS_HIP(hipMemcpy(&hi, all[i], sizeof(hi), hipMemcpyDeviceToHost));
+    DGS_HIP(hipFree(all[i]));
+    if (i == rank_) continue;
+    DGS_HIP(hipIpcOpenMemHandle(&ptrs_[i], hi, hipIpcMemLazyEnablePeerAccess));
+  }
+}
+
+P2PServer::~P2PServer() {
+  try {
+    if (world_ > 1)
+      for (int i = 0; i < world_; ++i)
+        if (i != rank_ && ptrs_[i]) (void)hipIpcCloseMemHandle(ptrs_[i]);
+    Comm::get().barrier();
+  } catch (...) {
+  }
+  if (!ptrs_.empty() && ptrs_[rank_]) (void)hipFree(ptrs_[rank_]);
+}
+
+// Rotation order of hashmap.cu:37-72: remote ranks (local+1, local+2, ...) then local last,
+// later writers win -- a node cached on several GPUs is read from the local one if present.
+static std::vector<int> rotation(int rank, int world) {
+  std::vector<int> order;
+  for (int d = 0; d < world; ++d) {
+    const int idx = (d + rank) % world;
+    if (idx != rank) order.push_back(idx);
+  }
+  order.push_back(rank);
+  return order;
+}
+
+static int64_t *device_copy_ids(const int64_t *ids, int64_t n, hipStream_t st) {
+  int64_t *d = nullptr;
+  DGS_HIP(hipMalloc(&d, sizeof(int64_t) * (size_t)(n > 0 ? n : 1)));
+  if (n > 0) DGS_HIP(hipMemcpyAsync(d, ids, sizeof(int64_t) * n, hipMemcpyDefault, st));
+  return d;
+}
+
+// ============================================================== Sampler
+Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *probs,
+                 int64_t num_nodes, int64_t num_edges, const int64_t *cache_nids,
+                 int64_t n_cache, int64_t device_id) {
+  Comm &c = Comm::get();
+  rank_ = c.rank();
+  world_ = c.world();
+  DGS_CHECK(device_id == rank_, "device_id must equal the communicator rank (sampler.cc:72)");
+  DGS_CHECK(num_nodes >= 0 && num_edges >= 0 && n_cache >= 0, "negative sizes");
+  num_nodes_ = num_nodes;
+  num_edges_ = num_edges;
+  bias_ = probs != nullptr;
+  hipStream_t st = nullptr;
+  h_indptr_.attach(indptr, (num_nodes + 1) * 8);
+  h_indices_.attach(indices, num_edges * 8);
+  if (bias_) h_probs_.attach(probs, num_edges * 4);
+  const int64_t *d_indptr = (const int64_t *)h_indptr_.dev;
+
+  // this rank's cached sub-CSR (sampler.cc:89-110)
+  int64_t *nids = device_copy_ids(cache_nids, n_cache, st);
+  int64_t *sub_indptr = nullptr;
+  DGS_HIP(hipMalloc(&sub_indptr, sizeof(int64_t) * (size_t)(n_cache + 1)));
+  extract_indptr(nids, n_cache, d_indptr, sub_indptr, st);
+  int64_t n_sub = 0;
+  DGS_HIP(hipMemcpyAsync(&n_sub, sub_indptr + n_cache, sizeof(int64_t), hipMemcpyDeviceToHost,
+                         st));
+  DGS_HIP(hipStreamSynchronize(st));
+  void *sub_indices = nullptr, *sub_probs = nullptr;
+  DGS_HIP(hipMalloc(&sub_indices, sizeof(int64_t) * (size_t)(n_sub > 0 ? n_sub : 1)));
+  extract_edge_data(nids, n_cache, d_indptr, sub_indptr, h_indices_.dev, 8, sub_indices, st);
+  if (bias_) {
+    DGS_HIP(hipMalloc(&sub_probs, sizeof(float) * (size_t)(n_sub > 0 ? n_sub : 1)));
+    extract_edge_data(nids, n_cache, d_indptr, sub_indptr, h_probs_.dev, 4, sub_probs, st);
+  }
+  DGS_HIP(hipStreamSynchronize(st));
+  indptr_srv_ = P2PServer::adopt(sub_indptr, n_cache + 1, 8);
+  indices_srv_ = P2PServer::adopt(sub_indices, n_sub, 8);
+  if (bias_) probs_srv_ = P2PServer::adopt(sub_probs, n_sub, 4);
+  nids_srv_ = P2PServer::adopt(nids, n_cache, 8);
+
+  // graph shard context: node table (replaces CreateNidsP2PCacheHashMapCUDA, hashmap.cu)
+  ntab_.ensure(sizeof(NodeEntry) * (size_t)(num_nodes > 0 ? num_nodes : 1));
+  NodeEntry *ntab = ntab_.as<NodeEntry>();
+  ntab_init_host(ntab, d_indptr, num_nodes, st);
+  for (int d : rotation(rank_, world_))
+    ntab_assign(ntab, (const int64_t *)nids_srv_->ptr(d), (const int64_t *)indptr_srv_->ptr(d),
+                nids_srv_->items(d), d, st);
+  DGS_HIP(hipStreamSynchronize(st));
+
+  src_.ntab = ntab;
+  src_.indptr = nullptr;
+  for (int d = 0; d <= kMaxDevices; ++d) {
+    src_.indices.p[d] = nullptr;
+    src_.probs.p[d] = nullptr;
+  }
+  for (int d = 0; d < world_; ++d) {
+    src_.indices.p[d] = indices_srv_->ptr(d);
+    src_.probs.p[d] = bias_ ? probs_srv_->ptr(d) : nullptr;
+  }
+  src_.indices.p[kLocHost] = h_indices_.dev;
+  src_.probs.p[kLocHost] = bias_ ? h_probs_.dev : nullptr;
+}
+
+Sampler::~Sampler() {
+  delete indptr_srv_;
+  delete indices_srv_;
+  delete probs_srv_;
+  delete nids_srv_;
+}
+
+void Sampler::bounds(int64_t n_seeds, const int64_t *fan_out, int L, int64_t *fcap,
+                     int64_t *ecap) const {
+  int64_t s = n_seeds;
+  for (int h = 0; h < L; ++h) {
+    const int64_t k = fan_out[L - 1 - h];
+    const int64_t e = s * k;
+    ecap[h] = e;
+    s = s + e;
+    fcap[h] = s;
+  }
+}
+
+// sampler.cc:14-62, 146-166: hops run fan_out[L-1] .. fan_out[0]; seeds <- frontier.
+void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_out, int L,
+                     bool replace, int64_t *const *frontiers, int64_t *const *rows,
+                     int64_t *const *cols, int64_t *sizes, hipStream_t st) {
+  sizes_.ensure(4 * sizeof(int64_t));
+  ws_.host.ensure(4 * sizeof(int64_t));
+  int64_t *dsz = sizes_.as<int64_t>();
+  int64_t *hsz = ws_.host.as<int64_t>();
+  const int64_t *cur = seeds;
+  int64_t S = n_seeds;
+  for (int h = 0; h < L; ++h) {
+    const int64_t k = fan_out[L - 1 - h];
+    DGS_CHECK(k >= 0, "fan_out entries must be non-negative");
+    const uint64_t seed = rng().next();
+    const int64_t nnz_cap = S * k;
+    rowpos_.ensure(sizeof(int64_t) * (size_t)(nnz_cap > 0 ? nnz_cap : 1));
+    sample_hop(src_, cur, S, k, replace, bias_, seed, rowpos_.as<int64_t>(), cols[h], dsz, ws_,
+               st);
+    relabel_hop(cur, S, cols[h], dsz, nnz_cap, rowpos_.as<int64_t>(), frontiers[h], rows[h],
+                cols[h], dsz + 1, ws_, st);
+    DGS_HIP(hipMemcpyAsync(hsz, dsz, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    DGS_HIP(hipStreamSynchronize(st));
+    sizes[3 * h + 0] = S;
+    sizes[3 * h + 1] = hsz[1];
+    sizes[3 * h + 2] = hsz[0];
+    cur = frontiers[h];
+    S = hsz[1];
+  }
+}
+
+void Sampler::build_cache_rowtab(int64_t *tab, hipStream_t st) const {
+  ftab_init_host(tab, num_nodes_, st);
+  for (int d : rotation(rank_, world_))
+    ftab_assign(tab, (const int64_t *)nids_srv_->ptr(d), nids_srv_->items(d), d, st);
+}
+
+int64_t Sampler::cache_map_size() const {
+  int64_t n = 0;
+  for (int d = 0; d < world_; ++d) n += nids_srv_->items(d);
+  // upper bound before dedup; the exact count is produced by cache_map_fill's caller query
+  int64_t *tab = nullptr;
+  hipStream_t st = nullptr;
+  DGS_HIP(hipMalloc(&tab, sizeof(int64_t) * (size_t)(num_nodes_ > 0 ? num_nodes_ : 1)));
+  build_cache_rowtab(tab, st);
+  int64_t *cnt = nullptr;
+  DGS_HIP(hipMalloc(&cnt, sizeof(int64_t)));
+  cache_map_compact(tab, num_nodes_, nullptr, nullptr, nullptr, cnt, st);
+  DGS_HIP(hipMemcpy(&n, cnt, sizeof(int64_t), hipMemcpyDeviceToHost));
+  DGS_HIP(hipFree(cnt));
+  DGS_HIP(hipFree(tab));
+  return n;
+}
+
+void Sampler::cache_map_fill(int64_t *key, int64_t *idx, int64_t *devid, hipStream_t st) const {
+  int64_t *tab = nullptr, *cnt = nullptr;
+  DGS_HIP(hipMalloc(&tab, sizeof(int64_t) * (size_t)(num_nodes_ > 0 ? num_nodes_ : 1)));
+  DGS_HIP(hipMalloc(&cnt, sizeof(int64_t)));
+  build_cache_rowtab(tab, st);
+  cache_map_compact(tab, num_nodes_, key, idx, devid, cnt, st);
+  DGS_HIP(hipStreamSynchronize(st));
+  DGS_HIP(hipFree(cnt));
+  DGS_HIP(hipFree(tab));
+}
+
+// ============================================================== FeatureServer
+// feature_server.cc:10-61: cache rows = data[cache_nids] in this GPU's HBM, cache lists
+// all-gathered with RCCL (NCCLTensorAllGather_), node -> (GPU, row) map with local priority.
+FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_bytes,
+                             const int64_t *cache_nids, int64_t n_cache, int64_t device_id) {
+  Comm &c = Comm::get();
+  rank_ = c.rank();
+  world_ = c.world();
+  DGS_CHECK(device_id == rank_,
+            "device_id must equal the communicator rank (feature_server.cc:14)");
+  num_rows_ = num_rows;
+  row_bytes_ = row_bytes;
+  hipStream_t st = nullptr;
+  h_data_.attach(data, num_rows * row_bytes);
+  int64_t *nids = device_copy_ids(cache_nids, n_cache, st);
+  void *block = nullptr;
+  DGS_HIP(hipMalloc(&block, (size_t)(n_cache * row_bytes > 0 ? n_cache * row_bytes : 1)));
+  gather_plain(h_data_.dev, row_bytes, nids, 8, n_cache, block, st);
+  DGS_HIP(hipStreamSynchronize(st));
+  feat_srv_ = P2PServer::adopt(block, n_cache, row_bytes);
+
+  std::vector<int64_t> nbytes(world_, n_cache * 8);
+  std::vector<void *> lists(world_, nullptr);
+  if (world_ > 1) {
+    lists = c.allgather_device(nids, n_cache * 8, &nbytes);
+  } else {
+    lists[0] = nids;
+  }
+  ftab_.ensure(sizeof(int64_t) * (size_t)(num_rows > 0 ? num_rows : 1));
+  int64_t *ftab = ftab_.as<int64_t>();
+  ftab_init_host(ftab, num_rows, st);
+  for (int d : rotation(rank_, world_))
+    ftab_assign(ftab, (const int64_t *)lists[d], nbytes[d] / 8, d, st);
+  DGS_HIP(hipStreamSynchronize(st));
+  if (world_ > 1)
+    for (void *p : lists) DGS_HIP(hipFree(p));
+  DGS_HIP(hipFree(nids));
+  for (int d = 0; d <= kMaxDevices; ++d) bases_.p[d] = nullptr;
+  for (int d = 0; d < world_; ++d) bases_.p[d] = feat_srv_->ptr(d);
+  bases_.p[kLocHost] = h_data_.dev;
+}
+
+FeatureServer::~FeatureServer() { delete feat_srv_; }
+
+void FeatureServer::gather(const int64_t *nids, int64_t n, void *out, hipStream_t st) const {
+  gather_table(ftab_.as<int64_t>(), bases_, row_bytes_, nids, n, out, st);
+}
+
+}  // namespace dgs

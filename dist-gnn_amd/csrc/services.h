@@ -1,0 +1,105 @@
+// services.h -- stateful services behind the C ABI: TensorP2PServer, P2PCacheSampler,
+// P2PCacheFeatureServer (reference: src/cache/tensor_p2p_cache.*, src/sampling/sampler.*,
+// src/feature/feature_server.cc).
+#pragma once
+
+#include <vector>
+
+#include "context.h"
+#include "dgs_ops.h"
+
+namespace dgs {
+
+// A device block shared with every rank of the communicator through HIP IPC (one-sided
+// peer loads over xGMI).  Construction and destruction are collective when world > 1
+// (tensor_p2p_cache.cc:11-118).
+class P2PServer {
+ public:
+  // copies `items * item_bytes` bytes from src (device or host) into an owned block
+  P2PServer(const void *src, int64_t items, int64_t item_bytes);
+  // adopts an existing hipMalloc'd block
+  static P2PServer *adopt(void *block, int64_t items, int64_t item_bytes);
+  ~P2PServer();
+  void *ptr(int r) const { return ptrs_[r]; }
+  void *local() const { return ptrs_[rank_]; }
+  int64_t items(int r) const { return items_[r]; }
+  int64_t item_bytes() const { return item_bytes_; }
+  int world() const { return world_; }
+  int rank() const { return rank_; }
+
+ private:
+  P2PServer() = default;
+  void share();
+  std::vector<void *> ptrs_;
+  std::vector<int64_t> items_;
+  int64_t item_bytes_ = 0;
+  int rank_ = 0, world_ = 1;
+};
+
+// Registers host memory for the object's lifetime when the caller did not pin it.
+struct HostView {
+  const void *host = nullptr;
+  void *dev = nullptr;
+  bool registered_here = false;
+  void attach(const void *p, int64_t bytes) {
+    host = p;
+    dev = device_view(p, bytes, &registered_here);
+  }
+  ~HostView() {
+    if (registered_here) (void)hipHostUnregister(const_cast<void *>(host));
+  }
+};
+
+class Sampler {
+ public:
+  Sampler(const int64_t *indptr, const int64_t *indices, const float *probs, int64_t num_nodes,
+          int64_t num_edges, const int64_t *cache_nids, int64_t n_cache, int64_t device_id);
+  ~Sampler();
+  void bounds(int64_t n_seeds, const int64_t *fan_out, int L, int64_t *fcap,
+              int64_t *ecap) const;
+  void sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_out, int L,
+              bool replace, int64_t *const *frontiers, int64_t *const *rows,
+              int64_t *const *cols, int64_t *sizes, hipStream_t st);
+  const int64_t *sub_indptr() const { return (const int64_t *)indptr_srv_->local(); }
+  int64_t n_rows() const { return indptr_srv_->items(rank_) - 1; }
+  const int64_t *sub_indices() const { return (const int64_t *)indices_srv_->local(); }
+  int64_t n_edges() const { return indices_srv_->items(rank_); }
+  const float *sub_probs() const {
+    return probs_srv_ ? (const float *)probs_srv_->local() : nullptr;
+  }
+  int64_t cache_map_size() const;
+  void cache_map_fill(int64_t *key, int64_t *idx, int64_t *devid, hipStream_t st) const;
+
+ private:
+  void build_cache_rowtab(int64_t *tab, hipStream_t st) const;
+  int64_t num_nodes_ = 0, num_edges_ = 0;
+  int rank_ = 0, world_ = 1;
+  bool bias_ = false;
+  HostView h_indptr_, h_indices_, h_probs_;
+  P2PServer *indptr_srv_ = nullptr, *indices_srv_ = nullptr, *probs_srv_ = nullptr;
+  P2PServer *nids_srv_ = nullptr;
+  DevBuf ntab_;
+  RowSrc src_{};
+  HopScratch ws_;
+  DevBuf rowpos_, sizes_;
+};
+
+class FeatureServer {
+ public:
+  FeatureServer(const void *data, int64_t num_rows, int64_t row_bytes, const int64_t *cache_nids,
+                int64_t n_cache, int64_t device_id);
+  ~FeatureServer();
+  void gather(const int64_t *nids, int64_t n, void *out, hipStream_t st) const;
+  const void *local() const { return feat_srv_ ? feat_srv_->local() : nullptr; }
+  int64_t local_rows() const { return feat_srv_ ? feat_srv_->items(rank_) : 0; }
+
+ private:
+  int64_t num_rows_ = 0, row_bytes_ = 0;
+  int rank_ = 0, world_ = 1;
+  HostView h_data_;
+  P2PServer *feat_srv_ = nullptr;
+  DevBuf ftab_;
+  PtrTable bases_{};
+};
+
+}  // namespace dgs

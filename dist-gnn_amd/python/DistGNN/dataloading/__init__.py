@@ -1,0 +1,3 @@
+from .dataloader import *  # noqa: F401,F403
+from .load_dataset import *  # noqa: F401,F403
+from .synthetic import *  # noqa: F401,F403

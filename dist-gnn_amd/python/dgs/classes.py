@@ -1,0 +1,197 @@
+"""dgs.classes -- mirror of the reference's `m_classes` submodule (src/pybind.cc:19-45):
+P2PCacheSampler, P2PCacheFeatureServer and TensorP2PServer with the same constructor
+arguments, method names (including the `_CAPI_sample_node_classifiction` spelling) and
+return shapes.  State lives in libdgs_amd.so; this layer only moves tensors across the C ABI.
+"""
+import ctypes
+
+import torch
+
+from ._lib import c_i64, c_vp, check, i64_array, lib, stream_ptr, vp_array
+from ._util import as_i64, check_cpu, check_cuda, device_view, ptr, row_bytes
+
+
+def _host_i64(t, name):
+    check_cpu(t, name)
+    return as_i64(t, name)
+
+
+class TensorP2PServer:
+    """tensor_p2p_cache.{h,cc}: a CUDA tensor copied into a library block and shared with
+    every rank through HIP IPC (collective when world_size > 1)."""
+
+    def __init__(self, tensor):
+        check_cuda(tensor, "tensor")
+        t = tensor.contiguous()
+        if t.dim() == 0 or t.shape[0] <= 0:
+            raise RuntimeError("TensorP2PServer needs at least one item")
+        self._shape = tuple(t.shape)
+        self._dtype = t.dtype
+        self._stride, item_bytes = row_bytes(t)
+        h = c_vp()
+        check(lib.dgs_p2p_server_create(ptr(t), t.shape[0], item_bytes, ctypes.byref(h)))
+        self._h = h
+
+    def _device(self, rank):
+        p, n = c_vp(), c_i64()
+        check(lib.dgs_p2p_server_device_ptr(self._h, int(rank), ctypes.byref(p), ctypes.byref(n)))
+        return p.value, n.value
+
+    def _CAPI_get_device_tensor(self, device_id):
+        """1-D view of items * stride elements (tensor_p2p_cache.cc:126-132)."""
+        p, n = self._device(device_id)
+        return device_view(p, (n * self._stride,), self._dtype, self)
+
+    def _CAPI_get_local_device_tensor(self):
+        p, _ = self._device(lib.dgs_get_local_rank())
+        return device_view(p, self._shape, self._dtype, self)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.dgs_p2p_server_destroy(h)
+            self._h = None
+
+
+class P2PCacheSampler:
+    """sampler.{h,cc}: multi-hop node-classification sampler over a host CSC graph with a
+    GPU-cached sub-CSR (local / peer GPUs) for `cache_nids`."""
+
+    def __init__(self, indptr, indices, probs, cache_nids, device_id):
+        for t, name in ((indptr, "indptr"), (indices, "indices"), (probs, "probs")):
+            check_cpu(t, name)
+        self._id_dtype = indices.dtype
+        self._cpu = (indptr, indices, probs)
+        ip = _host_i64(indptr, "indptr")
+        ix = _host_i64(indices, "indices")
+        self._keep = [ip, ix]
+        self.bias = probs.numel() > 0
+        pr = None
+        if self.bias:
+            if probs.dtype != torch.float32:
+                raise RuntimeError("probs must be float32")
+            pr = probs.contiguous()
+            self._keep.append(pr)
+        cn = cache_nids.to(torch.int64).contiguous()
+        self._keep.append(cn)
+        self.num_nodes = ip.numel() - 1
+        h = c_vp()
+        check(lib.dgs_sampler_create(ptr(ip), ptr(ix), ptr(pr), self.num_nodes, ix.numel(),
+                                     ptr(cn), cn.numel(), int(device_id), ctypes.byref(h)))
+        self._h = h
+        self.device = torch.device("cuda", torch.cuda.current_device())
+
+    def _CAPI_sample_node_classifiction(self, seeds, fan_out, replace=False):
+        """sampler.cc:146-166 -> [(seeds, frontier, coo_row, coo_col)] per hop
+        (hop h samples fan_out[L-1-h]); coo ids are local to (frontier, seeds)."""
+        check_cuda(seeds, "seeds")
+        s = as_i64(seeds, "seeds")
+        L = len(fan_out)
+        if L == 0:
+            return []
+        fo = i64_array(fan_out)
+        fcap, ecap = (c_i64 * L)(), (c_i64 * L)()
+        check(lib.dgs_sampler_bounds(self._h, s.numel(), fo, L, fcap, ecap))
+        dev = s.device
+        fronts = [torch.empty(int(fcap[h]), dtype=torch.int64, device=dev) for h in range(L)]
+        rows = [torch.empty(int(ecap[h]), dtype=torch.int64, device=dev) for h in range(L)]
+        cols = [torch.empty(int(ecap[h]), dtype=torch.int64, device=dev) for h in range(L)]
+        sizes = (c_i64 * (3 * L))()
+        check(lib.dgs_sampler_sample(self._h, ptr(s), s.numel(), fo, L, int(bool(replace)),
+                                     vp_array([t.data_ptr() for t in fronts]),
+                                     vp_array([t.data_ptr() for t in rows]),
+                                     vp_array([t.data_ptr() for t in cols]), sizes,
+                                     stream_ptr(dev)))
+        out = []
+        cur = seeds
+        cast = self._id_dtype != torch.int64
+        for h in range(L):
+            U, nnz = int(sizes[3 * h + 1]), int(sizes[3 * h + 2])
+            fr, r, c = fronts[h][:U], rows[h][:nnz], cols[h][:nnz]
+            if cast:
+                fr, r, c = fr.to(self._id_dtype), r.to(self._id_dtype), c.to(self._id_dtype)
+            out.append((cur, fr, r, c))
+            cur = fr
+        return out
+
+    def _CAPI_get_cpu_structure_tensors(self):
+        indptr, indices, probs = self._cpu
+        return indptr, indices, (probs if self.bias else None)
+
+    def _CAPI_get_local_cache_structure_tensors(self):
+        """Non-owning device views of this rank's cached sub-CSR (sampler.cc:183-195)."""
+        pi, pe, pp = c_vp(), c_vp(), c_vp()
+        nr, ne = c_i64(), c_i64()
+        check(lib.dgs_sampler_local_cache(self._h, ctypes.byref(pi), ctypes.byref(nr),
+                                          ctypes.byref(pe), ctypes.byref(ne), ctypes.byref(pp)))
+        sub_indptr = device_view(pi.value, (nr.value + 1,), torch.int64, self)
+        sub_indices = device_view(pe.value, (ne.value,), torch.int64, self)
+        sub_probs = device_view(pp.value, (ne.value,), torch.float32, self) if self.bias else None
+        return sub_indptr, sub_indices, sub_probs
+
+    def _CAPI_get_local_cache_hashmap_tensors(self):
+        """(key, idx, devid) of every cached node, local entries first in priority
+        (hashmap.cu:37-72).  Compact nid-ordered form: the reference's open-addressing
+        layout is an implementation detail, only the lookup semantics are kept."""
+        n = c_i64()
+        check(lib.dgs_sampler_cache_map_size(self._h, ctypes.byref(n)))
+        key = torch.empty(n.value, dtype=torch.int64, device=self.device)
+        idx = torch.empty(n.value, dtype=torch.int64, device=self.device)
+        devid = torch.empty(n.value, dtype=torch.int64, device=self.device)
+        check(lib.dgs_sampler_cache_map_fill(self._h, ptr(key), ptr(idx), ptr(devid),
+                                             stream_ptr(self.device)))
+        return key, idx, devid
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.dgs_sampler_destroy(h)
+            self._h = None
+
+
+class P2PCacheFeatureServer:
+    """feature_server.cc: host feature matrix with a per-GPU HBM cache of `cache_nids`
+    rows, pooled across GPUs (peer rows are read one-sided over xGMI)."""
+
+    def __init__(self, data, cache_nids, device_id):
+        check_cpu(data, "data")
+        if data.dim() == 0:
+            raise RuntimeError("data must have at least one dimension")
+        self._cpu = data
+        d = data.contiguous()
+        self._keep = [d]
+        self._stride, self._row_bytes = row_bytes(d)
+        self._dtype = d.dtype
+        self._shape_tail = tuple(d.shape[1:])
+        cn = cache_nids.to(torch.int64).contiguous()
+        self._keep.append(cn)
+        h = c_vp()
+        check(lib.dgs_feature_server_create(ptr(d), d.shape[0], self._row_bytes, ptr(cn),
+                                            cn.numel(), int(device_id), ctypes.byref(h)))
+        self._h = h
+        self.device = torch.device("cuda", torch.cuda.current_device())
+
+    def _CAPI_get_cpu_feature(self):
+        return self._cpu
+
+    def _CAPI_get_gpu_feature(self):
+        p, n = c_vp(), c_i64()
+        check(lib.dgs_feature_server_local_cache(self._h, ctypes.byref(p), ctypes.byref(n)))
+        if not p.value:
+            return None
+        return device_view(p.value, (n.value,) + self._shape_tail, self._dtype, self)
+
+    def _CAPI_get_feature(self, nids):
+        """feature_server.cc:69-74 -> [n, stride] (2-D, feature_ops.cu:110-112)."""
+        check_cuda(nids, "nids")
+        n = as_i64(nids, "nids")
+        out = torch.empty((n.numel(), self._stride), dtype=self._dtype, device=n.device)
+        check(lib.dgs_feature_server_gather(self._h, ptr(n), n.numel(), ptr(out),
+                                            stream_ptr(n.device)))
+        return out
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.dgs_feature_server_destroy(h)
+            self._h = None

@@ -1,0 +1,239 @@
+"""dgs.ops -- mirror of the reference's `m_ops` submodule (src/pybind.cc:47-77).
+
+Every function keeps the reference name, argument order, dtype rules and return shape; the
+work is done by libdgs_amd.so (HIP kernels on the current device, current stream).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import c_i64, check, i64_array, lib, stream_ptr, vp_array
+from ._util import as_i64, check_cuda, ptr, row_bytes
+
+__all__ = [
+    "_CAPI_get_unique_id", "_CAPI_set_nccl", "_CAPI_compute_frontier_heat",
+    "_CAPI_compute_frontier_heat_with_bias", "_CAPI_tensor_pin_memory",
+    "_CAPI_tensor_unpin_memory", "_CAPI_cuda_sample_neighbors",
+    "_CAPI_cuda_sample_neighbors_bias", "_CAPI_cuda_sampled_tensor_relabel",
+    "_CAPI_cuda_index_select", "_Test_Randn", "_Test_NCCLTensorAllGather",
+    "_Test_GetLocalRank", "_Test_GetWorldSize", "_Test_ExtractEdgeData", "_Test_ExtractIndptr",
+    "_CAPI_set_random_seed",
+]
+
+_registered = {}
+
+
+def _cuda_dev():
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+# ------------------------------------------------------------------ communicator
+def _CAPI_get_unique_id():
+    """nccl_context.cc:13-18 -- RCCL unique id packed into 16 int64."""
+    out = (c_i64 * 16)()
+    check(lib.dgs_get_unique_id(out))
+    return [int(x) for x in out]
+
+
+def _CAPI_set_nccl(nranks, unique_id_array, rank):
+    """nccl_context.cc:20-45."""
+    ids = i64_array(unique_id_array)
+    check(lib.dgs_set_nccl(int(nranks), ids, len(unique_id_array), int(rank)))
+
+
+def _Test_GetLocalRank():
+    return int(lib.dgs_get_local_rank())
+
+
+def _Test_GetWorldSize():
+    return int(lib.dgs_get_world_size())
+
+
+def _Test_Randn():
+    """context/context.h:22-27 -- next launch seed (uint64)."""
+    return int(lib.dgs_randn_uint64())
+
+
+def _CAPI_set_random_seed(seed):
+    """ADDITIVE: reseed the launch-seed engine (std::mt19937_64) for reproducible sampling."""
+    check(lib.dgs_set_random_seed(int(seed) & 0xFFFFFFFFFFFFFFFF))
+
+
+def _Test_NCCLTensorAllGather(local_tensor):
+    """nccl_context.cc:52-112 -- sizes, then payload via grouped send/recv."""
+    check_cuda(local_tensor, "local_tensor")
+    t = local_tensor.contiguous()
+    world = _Test_GetWorldSize()
+    rank = _Test_GetLocalRank()
+    sizes = (c_i64 * world)()
+    check(lib.dgs_allgather_sizes(t.numel(), sizes))
+    out = [t if i == rank else torch.empty(int(sizes[i]), dtype=t.dtype, device=t.device)
+           for i in range(world)]
+    nbytes = i64_array([int(sizes[i]) * t.element_size() for i in range(world)])
+    check(lib.dgs_allgather_bytes(ptr(t), t.numel() * t.element_size(),
+                                  vp_array([o.data_ptr() for o in out]), nbytes, stream_ptr()))
+    return out
+
+
+# ------------------------------------------------------------------ pinning
+def _CAPI_tensor_pin_memory(data):
+    """pin_memory.cc:7-12 -- register the tensor's host storage (mapped) in place."""
+    if data.is_cuda or data.is_pinned() or data.numel() == 0:
+        return
+    p = data.data_ptr()
+    check(lib.dgs_host_register(ctypes.c_void_p(p), data.numel() * data.element_size()))
+    _registered[p] = data.numel() * data.element_size()
+
+
+def _CAPI_tensor_unpin_memory(data):
+    """pin_memory.cc:14-19.  The reference early-returns when is_pinned() (so it never
+    unregisters); here storage registered by _CAPI_tensor_pin_memory is released."""
+    if data.is_cuda:
+        return
+    p = data.data_ptr()
+    if p in _registered:
+        check(lib.dgs_host_unregister(ctypes.c_void_p(p)))
+        del _registered[p]
+
+
+# ------------------------------------------------------------------ sampling
+def _sample(seeds, indptr, indices, probs, num_picks, replace):
+    check_cuda(seeds, "seeds")
+    if seeds.dtype != indices.dtype:
+        raise RuntimeError("seeds dtype must equal indices dtype")
+    out_dtype = indices.dtype
+    s, ip, ix = as_i64(seeds, "seeds"), as_i64(indptr, "indptr"), as_i64(indices, "indices")
+    pr = None
+    if probs is not None:
+        if probs.dtype != torch.float32:
+            raise RuntimeError("probs must be float32")
+        pr = probs.contiguous()
+    cap = s.numel() * int(num_picks)
+    dev = seeds.device
+    row = torch.empty(max(cap, 0), dtype=torch.int64, device=dev)
+    col = torch.empty(max(cap, 0), dtype=torch.int64, device=dev)
+    nnz = c_i64(0)
+    check(lib.dgs_sample_neighbors(ptr(s), s.numel(), ptr(ip), ptr(ix), ptr(pr), int(num_picks),
+                                   int(bool(replace)), ptr(row), ptr(col), ctypes.byref(nnz),
+                                   stream_ptr(dev)))
+    row, col = row[:nnz.value], col[:nnz.value]
+    if out_dtype != torch.int64:
+        row, col = row.to(out_dtype), col.to(out_dtype)
+    return row, col
+
+
+def _CAPI_cuda_sample_neighbors(seeds, indptr, indices, num_picks, replace):
+    """rowwise_sampling.cu:143-189 -> (coo_row, coo_col)."""
+    return _sample(seeds, indptr, indices, None, num_picks, replace)
+
+
+def _CAPI_cuda_sample_neighbors_bias(seeds, indptr, indices, probs, num_picks, replace):
+    """rowwise_sampling_bias.cu:226-288 -> (coo_row, coo_col)."""
+    return _sample(seeds, indptr, indices, probs, num_picks, replace)
+
+
+def _CAPI_cuda_sampled_tensor_relabel(mapping_tensors, requiring_relabel_tensors):
+    """tensor_relabel.cu:182-205 -> (unique, [relabeled tensors])."""
+    maps = [as_i64(t, "mapping tensor") for t in mapping_tensors]
+    reqs = [as_i64(t, "relabel tensor") for t in requiring_relabel_tensors]
+    dtype = requiring_relabel_tensors[0].dtype if requiring_relabel_tensors else torch.int64
+    dev = maps[0].device if maps else _cuda_dev()
+    nm = sum(t.numel() for t in maps)
+    uniq = torch.empty(nm, dtype=torch.int64, device=dev)
+    outs = [torch.empty(t.numel(), dtype=torch.int64, device=dev) for t in reqs]
+    nu = c_i64(0)
+    check(lib.dgs_relabel(vp_array([t.data_ptr() for t in maps]),
+                          i64_array([t.numel() for t in maps]), len(maps),
+                          vp_array([t.data_ptr() for t in reqs]),
+                          i64_array([t.numel() for t in reqs]), len(reqs), ptr(uniq),
+                          ctypes.byref(nu), vp_array([o.data_ptr() for o in outs]),
+                          stream_ptr(dev)))
+    uniq = uniq[:nu.value]
+    if dtype != torch.int64:
+        uniq = uniq.to(dtype)
+        outs = [o.to(dtype) for o in outs]
+    outs = [o.view(r.shape) for o, r in zip(outs, requiring_relabel_tensors)]
+    return uniq, outs
+
+
+# ------------------------------------------------------------------ gather
+def _CAPI_cuda_index_select(data, nid):
+    """feature_ops.cu:173-210 -- out = data[nid] on the current CUDA device, keeping the
+    trailing shape; data may be a CUDA tensor or pinned host memory."""
+    if nid.dtype not in (torch.int32, torch.int64):
+        raise RuntimeError("ID can only be int32 or int64")
+    if data.dtype not in (torch.int32, torch.int64, torch.float32):
+        raise RuntimeError("Value can only be int32 or int64 or float32")
+    d = data.contiguous()
+    n = nid.contiguous()
+    _, rb = row_bytes(d)
+    dev = n.device if n.is_cuda else _cuda_dev()
+    out = torch.empty((n.numel(),) + tuple(d.shape[1:]), dtype=d.dtype, device=dev)
+    check(lib.dgs_index_select(ptr(d), rb, ptr(n), n.element_size(), n.numel(), ptr(out),
+                               stream_ptr(dev)))
+    return out
+
+
+# ------------------------------------------------------------------ cache helpers
+def _Test_ExtractIndptr(nids, indptr):
+    """utils.cu:12-42."""
+    n = as_i64(nids, "nids")
+    ip = as_i64(indptr, "indptr")
+    dev = n.device if n.is_cuda else _cuda_dev()
+    out = torch.empty(n.numel() + 1, dtype=torch.int64, device=dev)
+    check(lib.dgs_extract_indptr(ptr(n), n.numel(), ptr(ip), ptr(out), stream_ptr(dev)))
+    return out.to(indptr.dtype) if indptr.dtype != torch.int64 else out
+
+
+def _Test_ExtractEdgeData(nids, indptr, sub_indptr, edge_data):
+    """utils.cu:44-101."""
+    n = as_i64(nids, "nids")
+    ip = as_i64(indptr, "indptr")
+    sp = as_i64(sub_indptr, "sub_indptr")
+    ed = edge_data.contiguous()
+    total = int(sp[-1].item()) if sp.numel() else 0
+    dev = n.device if n.is_cuda else _cuda_dev()
+    out = torch.empty(total, dtype=ed.dtype, device=dev)
+    check(lib.dgs_extract_edge_data(ptr(n), n.numel(), ptr(ip), ptr(sp), ptr(ed),
+                                    ed.element_size(), ptr(out), stream_ptr(dev)))
+    return out
+
+
+# ------------------------------------------------------------------ heat
+def _heat(seeds, indptr, indices, probs, seeds_heat, num_picks, indptr_diff):
+    s, ip, ix = as_i64(seeds, "seeds"), as_i64(indptr, "indptr"), as_i64(indices, "indices")
+    if seeds_heat.dtype != torch.float32:
+        raise RuntimeError("heat must be float32")
+    fh = torch.zeros_like(seeds_heat)
+    pr = probs.contiguous() if probs is not None else None
+    check(lib.dgs_compute_frontier_heat(ptr(s), s.numel(), ptr(ip), ptr(ix), ptr(pr),
+                                        ptr(seeds_heat), seeds_heat.numel(), int(num_picks),
+                                        int(indptr_diff), ptr(fh), stream_ptr(fh.device)))
+    return fh
+
+
+def _CAPI_compute_frontier_heat(seeds, indptr, indices, seeds_heat, num_picks, indptr_diff):
+    """preprocess_heat.cu:35-56."""
+    return _heat(seeds, indptr, indices, None, seeds_heat, num_picks, indptr_diff)
+
+
+def _CAPI_compute_frontier_heat_with_bias(seeds, indptr, indices, probs, seeds_heat, num_picks,
+                                          indptr_diff):
+    """preprocess_heat.cu:100-121 (processes seeds.numel() - 1 seeds, as the reference)."""
+    return _heat(seeds, indptr, indices, probs, seeds_heat, num_picks, indptr_diff)
+
+
+def profile_enable(on=True):
+    check(lib.dgs_profile_enable(int(bool(on))))
+
+
+def profile_read():
+    gm, gn, sm, sn = ctypes.c_double(), c_i64(), ctypes.c_double(), c_i64()
+    check(lib.dgs_profile_read(ctypes.byref(gm), ctypes.byref(gn), ctypes.byref(sm),
+                               ctypes.byref(sn)))
+    return {"gather_ms": gm.value, "gather_launches": gn.value, "sample_ms": sm.value,
+            "sample_calls": sn.value}
+
+
+_lib  # noqa: B018  (keep module import for side effects)

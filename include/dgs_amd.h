@@ -1,0 +1,181 @@
+/*
+ * dgs_amd.h -- C ABI of the DGS-AMD sampling / feature-gather library (libdgs_amd.so).
+ *
+ * This is the drop-in boundary for the hot path of CommediaJW/Dist-GNN: every entry point
+ * replaces one binding of the reference's pybind11 module `dgs` (src/pybind.cc:17-77) or
+ * the service method behind it.  Signatures use plain pointers and sizes only -- no torch
+ * types.  The Python package `dgs` (dist-gnn_amd/python/dgs, a ctypes binding) mirrors the
+ * reference module layout on top of these functions; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Every function returns 0 on success and -1 on error; dgs_last_error() then returns a
+ *    thread-local message.  (The reference calls exit()/abort() on CUDA/NCCL errors,
+ *    dgs_headers.h:11-34; DGS-AMD reports instead.)
+ *  - `stream` is a hipStream_t (NULL = the legacy default stream, which is what the
+ *    reference launches on).  Calls are stream-ordered; calls that must return a size
+ *    computed on the device (marked SYNC) synchronise `stream` once.
+ *  - Device arrays: pointers usable by the current HIP device (device memory, or host
+ *    memory registered with dgs_host_register / allocated pinned).
+ *  - Ids and CSR offsets are int64 unless an `*_bytes` argument says otherwise.
+ */
+#ifndef DGS_AMD_H_
+#define DGS_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char *dgs_last_error(void);
+/* Library build identification (gfx target and version string). */
+const char *dgs_version(void);
+
+/* ------------------------------------------------------------------------------------
+ * Context: communicator and launch-seed RNG (src/nccl/nccl_context.{h,cc}, src/context)
+ * ---------------------------------------------------------------------------------- */
+/* replaces nccl::GetUniqueId (nccl_context.cc:13-18; pybind.cc:50). out[16] */
+int dgs_get_unique_id(int64_t *out_id16);
+/* replaces nccl::SetNCCL / NCCLContext::SetNCCL_ (nccl_context.cc:20-45; pybind.cc:51) */
+int dgs_set_nccl(int64_t nranks, const int64_t *unique_id, int64_t n_id, int64_t rank);
+/* replaces _Test_GetLocalRank / _Test_GetWorldSize (nccl_context.cc:31-32; pybind.cc:72-73).
+ * Before dgs_set_nccl they report rank 0 of 1. */
+int dgs_get_local_rank(void);
+int dgs_get_world_size(void);
+/* replaces NCCLContext::Barrier_ (nccl_context.cc:46-50): 1-float all-reduce + sync */
+int dgs_barrier(void);
+/* replaces NCCLContext::NCCLTensorAllGather_ (nccl_context.cc:52-112), split in the two
+ * phases the reference runs: sizes (8 B per rank) then payload via grouped send/recv. */
+int dgs_allgather_sizes(int64_t my_size, int64_t *all_sizes /* [world] host */);
+int dgs_allgather_bytes(const void *send, int64_t send_bytes, void *const *recv /* [world] */,
+                        const int64_t *recv_bytes /* [world] */, void *stream);
+/* replaces ctx::randn_uint64 (context/context.h:22-27; pybind.cc:71 _Test_Randn) */
+uint64_t dgs_randn_uint64(void);
+/* ADDITIVE (not in the reference): reseed the launch-seed engine (std::mt19937_64) so that
+ * sampling is reproducible; the reference seeds it from std::random_device
+ * (context/context.h:9-10). */
+int dgs_set_random_seed(uint64_t seed);
+
+/* ------------------------------------------------------------------------------------
+ * Host memory registration (src/common/pin_memory.cc:7-19; pybind.cc:57-58)
+ * ---------------------------------------------------------------------------------- */
+int dgs_host_register(void *ptr, int64_t bytes);
+int dgs_host_unregister(void *ptr);
+
+/* ------------------------------------------------------------------------------------
+ * Stateless ops (pybind.cc:53-76)
+ * ---------------------------------------------------------------------------------- */
+/* replaces feature::cuda::GetFeaturesCUDA (feature_ops.cu:140-210; _CAPI_cuda_index_select):
+ * out[i, :] = data[nid[i], :] as a byte copy of row_bytes per row. nid_bytes = 4 | 8. */
+int dgs_index_select(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
+                     int64_t n, void *out, void *stream);
+
+/* replaces sampling::cuda::RowWiseSamplingUniformCUDA (rowwise_sampling.cu:143-189) and,
+ * when probs != NULL, RowWiseSamplingBiasCUDA (rowwise_sampling_bias.cu:226-288)
+ * (_CAPI_cuda_sample_neighbors / _CAPI_cuda_sample_neighbors_bias).  Draws one launch seed
+ * from the context RNG.  out_row/out_col capacity: S * num_picks.  SYNC: *nnz_out. */
+int dgs_sample_neighbors(const int64_t *seeds, int64_t S, const int64_t *indptr,
+                         const int64_t *indices, const float *probs, int64_t num_picks,
+                         int replace, int64_t *out_row, int64_t *out_col, int64_t *nnz_out,
+                         void *stream);
+
+/* replaces sampling::cuda::TensorRelabelCUDA (tensor_relabel.cu:182-205;
+ * _CAPI_cuda_sampled_tensor_relabel).  unique_out capacity: sum(map_sizes).
+ * req_out[j] receives the relabeled req[j].  SYNC: *n_unique. */
+int dgs_relabel(const int64_t *const *maps, const int64_t *map_sizes, int n_maps,
+                const int64_t *const *reqs, const int64_t *req_sizes, int n_reqs,
+                int64_t *unique_out, int64_t *n_unique, int64_t *const *req_out, void *stream);
+
+/* replaces sampling::cuda::ExtractIndptr (utils.cu:12-42; _Test_ExtractIndptr) */
+int dgs_extract_indptr(const int64_t *nids, int64_t n, const int64_t *indptr,
+                       int64_t *sub_indptr /* [n+1] */, void *stream);
+/* replaces sampling::cuda::ExtractEdgeData (utils.cu:44-101; _Test_ExtractEdgeData) */
+int dgs_extract_edge_data(const int64_t *nids, int64_t n, const int64_t *indptr,
+                          const int64_t *sub_indptr, const void *edge_data, int64_t elem_bytes,
+                          void *sub_edge_data, void *stream);
+
+/* replaces cache::cuda::ComputeFrontierHeat[WithBias] (preprocess_heat.cu:35-56,100-121;
+ * _CAPI_compute_frontier_heat[_with_bias]).  probs == NULL selects the unbiased form.
+ * frontier_heat[num_nodes] is overwritten. */
+int dgs_compute_frontier_heat(const int64_t *seeds, int64_t n_seeds, const int64_t *indptr,
+                              const int64_t *indices, const float *probs,
+                              const float *seeds_heat, int64_t num_nodes, int64_t num_picks,
+                              int64_t indptr_diff, float *frontier_heat, void *stream);
+
+/* ------------------------------------------------------------------------------------
+ * TensorP2PServer (src/cache/tensor_p2p_cache.{h,cc}; pybind.cc:41-45)
+ * ---------------------------------------------------------------------------------- */
+typedef struct dgs_p2p_server dgs_p2p_server;
+/* Copies `bytes` from `src` (device or registered host) into a block owned by the server,
+ * exports it to every rank (collective when world_size > 1). item_bytes = bytes per item. */
+int dgs_p2p_server_create(const void *src, int64_t items, int64_t item_bytes,
+                          dgs_p2p_server **out);
+int dgs_p2p_server_device_ptr(dgs_p2p_server *s, int64_t rank, void **ptr, int64_t *items);
+int dgs_p2p_server_destroy(dgs_p2p_server *s); /* collective when world_size > 1 */
+
+/* ------------------------------------------------------------------------------------
+ * P2PCacheSampler (src/sampling/sampler.{h,cc}; pybind.cc:21-31)
+ * ---------------------------------------------------------------------------------- */
+typedef struct dgs_sampler dgs_sampler;
+/* indptr[num_nodes+1], indices[num_edges], probs[num_edges] or NULL: host arrays (registered
+ * by the library when not already pinned) -- sampler.cc:64-136.  cache_nids: this rank's
+ * cached node ids (device or host).  Collective when world_size > 1. */
+int dgs_sampler_create(const int64_t *indptr, const int64_t *indices, const float *probs,
+                       int64_t num_nodes, int64_t num_edges, const int64_t *cache_nids,
+                       int64_t n_cache, int64_t device_id, dgs_sampler **out);
+/* Upper bounds for the per-hop output buffers of dgs_sampler_sample:
+ * frontier_cap[h], edge_cap[h] for h = 0..L-1 (hop h uses fan_out[L-1-h]). */
+int dgs_sampler_bounds(const dgs_sampler *s, int64_t n_seeds, const int64_t *fan_out, int L,
+                       int64_t *frontier_cap, int64_t *edge_cap);
+/* replaces P2PCacheSampler::NodeClassifictionSample (sampler.cc:146-166): hop h writes the
+ * frontier (unique(seeds_h ++ sampled cols), first-occurrence order) to frontiers[h] and the
+ * relabeled COO to rows[h]/cols[h]; sizes_out[3h..3h+2] = (S_h, |frontier_h|, nnz_h).
+ * SYNC (once per hop). */
+int dgs_sampler_sample(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
+                       const int64_t *fan_out, int L, int replace, int64_t *const *frontiers,
+                       int64_t *const *rows, int64_t *const *cols, int64_t *sizes_out,
+                       void *stream);
+/* _CAPI_get_local_cache_structure_tensors (sampler.cc:183-195): non-owning device views. */
+int dgs_sampler_local_cache(const dgs_sampler *s, const int64_t **sub_indptr, int64_t *n_rows,
+                            const int64_t **sub_indices, int64_t *n_edges,
+                            const float **sub_probs);
+/* _CAPI_get_local_cache_hashmap_tensors (sampler.cc:197-201): the (nid, row, device) map of
+ * every cached node, local entries taking priority (hashmap.cu:37-72).  Two-step: query
+ * the count, then fill caller buffers (device). */
+int dgs_sampler_cache_map_size(const dgs_sampler *s, int64_t *n);
+int dgs_sampler_cache_map_fill(const dgs_sampler *s, int64_t *key, int64_t *idx,
+                               int64_t *devid, void *stream);
+int dgs_sampler_destroy(dgs_sampler *s); /* collective when world_size > 1 */
+
+/* ------------------------------------------------------------------------------------
+ * P2PCacheFeatureServer (src/feature/feature_server.cc, feature_sever.h; pybind.cc:33-39)
+ * ---------------------------------------------------------------------------------- */
+typedef struct dgs_feature_server dgs_feature_server;
+/* data: host array [num_rows, row_bytes] (registered by the library when not pinned);
+ * cache_nids: rows cached in this GPU's HBM (device or host).  feature_server.cc:10-61. */
+int dgs_feature_server_create(const void *data, int64_t num_rows, int64_t row_bytes,
+                              const int64_t *cache_nids, int64_t n_cache, int64_t device_id,
+                              dgs_feature_server **out);
+/* replaces P2PCacheFeatureServer::GetFeatures (feature_server.cc:69-74) and
+ * GetFeaturesP2PCacheCUDA (feature_ops.cu:75-138): out[i,:] = X[nids[i],:] from the local
+ * cache, a peer's cache (xGMI) or host memory, in one fused lookup+gather kernel. */
+int dgs_feature_server_gather(dgs_feature_server *s, const int64_t *nids, int64_t n,
+                              void *out, void *stream);
+int dgs_feature_server_local_cache(const dgs_feature_server *s, const void **ptr,
+                                   int64_t *rows);
+int dgs_feature_server_destroy(dgs_feature_server *s);
+
+/* ------------------------------------------------------------------------------------
+ * Instrumentation (bench.py): time the hot kernels with HIP events on the stream they run
+ * on.  When enabled, the library records events around its gather kernel and sums their
+ * durations; dgs_profile_read() returns (total_ms, launches) and resets.
+ * ---------------------------------------------------------------------------------- */
+int dgs_profile_enable(int on);
+int dgs_profile_read(double *gather_ms, int64_t *gather_launches, double *sample_ms,
+                     int64_t *sample_calls);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DGS_AMD_H_ */

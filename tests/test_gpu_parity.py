@@ -1,0 +1,309 @@
+"""GPU parity: the HIP path (libdgs_amd.so through the `dgs` binding) against the CPU oracle.
+
+Bar: bit-exact for sampled indices, frontiers, relabeled COO and every gather (a byte copy);
+the heat ops use float atomics in the reference, so they are compared with rtol 1e-5.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def dgs():
+    import dgs as _dgs
+    return _dgs
+
+
+def _gold():
+    return np.load(os.path.join(GOLD, "sampler_golden.npz"))
+
+
+def _hub_graph(seed=0):
+    """Small graph with degree-0 rows, deg == k rows and hub rows (deg >> 1024 + k)."""
+    rng = np.random.default_rng(seed)
+    n = 400
+    degs = rng.integers(0, 80, n)
+    degs[:6] = [0, 1, 5, 15, 3000, 9000]
+    degs[6:10] = [130, 512, 1040, 1100]
+    indptr = np.concatenate([[0], np.cumsum(degs)]).astype(np.int64)
+    indices = rng.integers(0, n, int(indptr[-1])).astype(np.int64)
+    probs = (rng.random(indices.size) + 0.01).astype(np.float32)
+    probs[::13] = 0.0
+    return indptr, indices, probs
+
+
+def _cuda(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+# ------------------------------------------------------------------ gather
+@pytest.mark.parametrize("dim", [1, 3, 100, 128, 256, 257])
+@pytest.mark.parametrize("nid_dtype", [torch.int64, torch.int32])
+def test_index_select_matches_oracle(dgs, dim, nid_dtype):
+    rng = np.random.default_rng(dim)
+    data = rng.standard_normal((5000, dim)).astype(np.float32)
+    nids = rng.integers(0, 5000, 7777)
+    got = dgs.ops._CAPI_cuda_index_select(_cuda(data), _cuda(nids, nid_dtype))
+    exp = O.index_select(data, nids)
+    assert got.shape == (7777, dim)
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), exp.view(np.uint32))
+
+
+def test_index_select_labels_pinned_host(dgs):
+    labels = torch.arange(1000, dtype=torch.int64) * 7
+    labels = labels.pin_memory()
+    nids = torch.randint(0, 1000, (333,), device="cuda")
+    got = dgs.ops._CAPI_cuda_index_select(labels, nids)
+    assert got.is_cuda and torch.equal(got.cpu(), labels[nids.cpu()])
+    lab3 = torch.arange(3000, dtype=torch.float32).reshape(1000, 3)
+    dgs.ops._CAPI_tensor_pin_memory(lab3)
+    got = dgs.ops._CAPI_cuda_index_select(lab3, nids)
+    assert torch.equal(got.cpu(), lab3[nids.cpu()])
+    dgs.ops._CAPI_tensor_unpin_memory(lab3)
+
+
+def test_index_select_empty(dgs):
+    data = torch.randn(10, 4, device="cuda")
+    out = dgs.ops._CAPI_cuda_index_select(data, torch.empty(0, dtype=torch.int64, device="cuda"))
+    assert out.shape == (0, 4)
+
+
+# ------------------------------------------------------------------ standalone sampling
+@pytest.mark.parametrize("k", [1, 5, 15, 40, 130])
+@pytest.mark.parametrize("replace", [False, True])
+def test_sample_neighbors_uniform(dgs, k, replace):
+    indptr, indices, _ = _hub_graph(k)
+    seeds = np.random.default_rng(k).permutation(indptr.size - 1)[:300]
+    seeds = np.concatenate([np.arange(10), seeds])
+    for s in (1, 2):
+        dgs.ops._CAPI_set_random_seed(1000 * k + s)
+        ls = O.launch_seeds(1000 * k + s, 1)[0]
+        row, col = dgs.ops._CAPI_cuda_sample_neighbors(_cuda(seeds), _cuda(indptr),
+                                                       _cuda(indices), k, replace)
+        er, ec = O.sample_uniform(seeds, indptr, indices, k, replace, ls)
+        assert np.array_equal(row.cpu().numpy(), er)
+        assert np.array_equal(col.cpu().numpy(), ec)
+
+
+@pytest.mark.parametrize("k", [1, 4, 15, 32])
+@pytest.mark.parametrize("replace", [False, True])
+def test_sample_neighbors_bias(dgs, k, replace):
+    indptr, indices, probs = _hub_graph(7 + k)
+    seeds = np.concatenate([np.arange(10), np.random.default_rng(k).integers(0, 400, 200)])
+    dgs.ops._CAPI_set_random_seed(77 + k)
+    ls = O.launch_seeds(77 + k, 1)[0]
+    row, col = dgs.ops._CAPI_cuda_sample_neighbors_bias(_cuda(seeds), _cuda(indptr),
+                                                        _cuda(indices), _cuda(probs), k, replace)
+    er, ec = O.sample_bias(seeds, indptr, indices, probs, k, replace, ls)
+    assert np.array_equal(row.cpu().numpy(), er)
+    assert np.array_equal(col.cpu().numpy(), ec)
+
+
+def test_sample_golden_vectors(dgs):
+    z = _gold()
+    seeds, indptr, indices, probs = z["seeds"], z["indptr"], z["indices"], z["probs"]
+    # the fixture's launch seeds are mt19937_64(7) outputs 0..15
+    i = 0
+    for k in (3, 5, 15, 40):
+        for rep in (0, 1):
+            dgs.ops._CAPI_set_random_seed(7)
+            for _ in range(i % 16):
+                dgs.ops._Test_Randn()
+            r, c = dgs.ops._CAPI_cuda_sample_neighbors(_cuda(seeds), _cuda(indptr),
+                                                       _cuda(indices), k, bool(rep))
+            assert np.array_equal(r.cpu().numpy(), z[f"uniform_k{k}_r{rep}_row"])
+            assert np.array_equal(c.cpu().numpy(), z[f"uniform_k{k}_r{rep}_col"])
+            if k <= 32:
+                dgs.ops._CAPI_set_random_seed(7)
+                for _ in range(i % 16):
+                    dgs.ops._Test_Randn()
+                r, c = dgs.ops._CAPI_cuda_sample_neighbors_bias(
+                    _cuda(seeds), _cuda(indptr), _cuda(indices), _cuda(probs), k, bool(rep))
+                assert np.array_equal(r.cpu().numpy(), z[f"bias_k{k}_r{rep}_row"])
+                assert np.array_equal(c.cpu().numpy(), z[f"bias_k{k}_r{rep}_col"])
+            i += 1
+
+
+def test_sample_empty_and_zero_picks(dgs):
+    indptr, indices, _ = _hub_graph()
+    e = torch.empty(0, dtype=torch.int64, device="cuda")
+    r, c = dgs.ops._CAPI_cuda_sample_neighbors(e, _cuda(indptr), _cuda(indices), 5, False)
+    assert r.numel() == 0 and c.numel() == 0
+    s = _cuda(np.arange(20))
+    r, c = dgs.ops._CAPI_cuda_sample_neighbors(s, _cuda(indptr), _cuda(indices), 0, False)
+    assert r.numel() == 0
+
+
+# ------------------------------------------------------------------ relabel
+def test_relabel_matches_oracle(dgs):
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 17, 5000):
+        a = rng.integers(0, 300, n)
+        b = rng.integers(0, 600, 3 * n)
+        uniq, (ra, rb) = dgs.ops._CAPI_cuda_sampled_tensor_relabel([_cuda(a), _cuda(b)],
+                                                                  [_cuda(a), _cuda(b)])
+        eu, (ea, eb) = O.relabel([a, b], [a, b])
+        assert np.array_equal(uniq.cpu().numpy(), eu)
+        assert np.array_equal(ra.cpu().numpy(), ea) and np.array_equal(rb.cpu().numpy(), eb)
+    uniq, (r,) = dgs.ops._CAPI_cuda_sampled_tensor_relabel([_cuda([5, 6])], [_cuda([6, 7, 5])])
+    assert uniq.tolist() == [5, 6] and r.tolist() == [1, -1, 0]
+
+
+# ------------------------------------------------------------------ extract / KATs
+def test_reference_extract_kat(dgs):
+    with open(os.path.join(GOLD, "reference_kats.json")) as f:
+        k = json.load(f)
+    g, e = k["toy_graph"], k["extract"]
+    indptr = torch.tensor(g["indptr"]).cuda()
+    nids = torch.tensor(e["cache_nids"]).cuda()
+    sub = dgs.ops._Test_ExtractIndptr(nids, indptr)
+    assert sub.tolist() == e["sub_indptr"]
+    assert dgs.ops._Test_ExtractEdgeData(nids, indptr, sub,
+                                         torch.tensor(g["indices"]).cuda()).tolist() == \
+        e["sub_indices"]
+    probs = torch.tensor(g["probs"], dtype=torch.float32).cuda()
+    assert torch.equal(dgs.ops._Test_ExtractEdgeData(nids, indptr, sub, probs).cpu(),
+                       torch.tensor(e["sub_probs"], dtype=torch.float32))
+    for nids_r, exp in zip(k["p2p_server"]["rank_cache_nids"], k["p2p_server"]["rank_sub_indptr"]):
+        assert dgs.ops._Test_ExtractIndptr(torch.tensor(nids_r).cuda(), indptr).tolist() == exp
+
+
+def test_reference_feature_server_kat(dgs):
+    with open(os.path.join(GOLD, "reference_kats.json")) as f:
+        k = json.load(f)["feature_server"]
+    feat = torch.arange(0, 100, 1).float().pin_memory().reshape(10, 10)
+    fs = dgs.classes.P2PCacheFeatureServer(feat, torch.tensor(k["rank_cache_nids"][0]).cuda(), 0)
+    got = fs._CAPI_get_feature(torch.tensor(k["query"]).cuda())
+    assert got.tolist() == [[float(x) for x in row] for row in k["expected"]]
+    assert torch.equal(fs._CAPI_get_cpu_feature(), feat)
+    assert torch.equal(fs._CAPI_get_gpu_feature().cpu(), feat[[0, 3]])
+
+
+# ------------------------------------------------------------------ services
+@pytest.mark.parametrize("cache", ["all", "half", "none_but_one"])
+@pytest.mark.parametrize("replace", [False, True])
+@pytest.mark.parametrize("bias", [False, True])
+def test_p2p_cache_sampler_matches_oracle(dgs, cache, replace, bias):
+    indptr, indices, probs = _hub_graph(11)
+    n = indptr.size - 1
+    if cache == "all":
+        cnids = np.random.default_rng(0).permutation(n)
+    elif cache == "half":
+        cnids = np.random.default_rng(1).permutation(n)[: n // 2]
+    else:
+        cnids = np.array([3])
+    pr = torch.from_numpy(probs) if bias else torch.Tensor()
+    sampler = dgs.classes.P2PCacheSampler(torch.from_numpy(indptr), torch.from_numpy(indices), pr,
+                                          torch.from_numpy(cnids), 0)
+    seeds = np.random.default_rng(5).permutation(n)[:64]
+    seeds[:6] = np.arange(6)
+    fan_out = [15, 10, 5] if not bias else [8, 5, 3]
+    dgs.ops._CAPI_set_random_seed(4242)
+    got = sampler._CAPI_sample_node_classifiction(_cuda(seeds), fan_out, replace)
+    exp = O.node_classification_sample(seeds, indptr, indices, fan_out, replace,
+                                       O.launch_seeds(4242, 3), probs=probs if bias else None)
+    assert len(got) == len(exp) == 3
+    for (gs, gf, gr, gc), (es, ef, er, ec) in zip(got, exp):
+        assert np.array_equal(gs.cpu().numpy(), es)
+        assert np.array_equal(gf.cpu().numpy(), ef)
+        assert np.array_equal(gr.cpu().numpy(), er)
+        assert np.array_equal(gc.cpu().numpy(), ec)
+
+
+def test_sampler_getters(dgs):
+    with open(os.path.join(GOLD, "reference_kats.json")) as f:
+        g = json.load(f)["toy_graph"]
+    indptr = torch.tensor(g["indptr"]).pin_memory()
+    indices = torch.tensor(g["indices"]).pin_memory()
+    probs = torch.tensor(g["probs"]).pin_memory()
+    s = dgs.classes.P2PCacheSampler(indptr, indices, probs, torch.tensor([0, 3]), 0)
+    ip, ix, pr = s._CAPI_get_cpu_structure_tensors()
+    assert ip is indptr and ix is indices and pr is probs
+    si, sx, sp = s._CAPI_get_local_cache_structure_tensors()
+    assert si.tolist() == [0, 4, 4] and sx.tolist() == [1, 2, 3, 4]
+    assert torch.allclose(sp.cpu(), torch.tensor([0.1, 0.2, 0.3, 0.4]))
+    key, idx, devid = s._CAPI_get_local_cache_hashmap_tensors()
+    assert key.tolist() == [0, 3] and idx.tolist() == [0, 1] and devid.tolist() == [0, 0]
+    # reference test_sampler_bias.py: seeds [0, 3, 5], fan-out [2, 2]
+    res = s._CAPI_sample_node_classifiction(torch.tensor([0, 3, 5]).cuda(), [2, 2], False)
+    assert res[0][1][:3].tolist() == [0, 3, 5]
+
+
+def test_feature_server_matches_oracle(dgs):
+    rng = np.random.default_rng(9)
+    data = rng.standard_normal((3000, 100)).astype(np.float32)
+    for cnids in (np.arange(3000), rng.permutation(3000)[:1000], np.array([7])):
+        fs = dgs.classes.P2PCacheFeatureServer(torch.from_numpy(data), torch.from_numpy(cnids), 0)
+        q = rng.integers(0, 3000, 4096)
+        got = fs._CAPI_get_feature(_cuda(q))
+        assert np.array_equal(got.cpu().numpy(), O.index_select(data, q))
+
+
+def test_tensor_p2p_server_local(dgs):
+    t = torch.arange(12, dtype=torch.int64, device="cuda").reshape(4, 3)
+    srv = dgs.classes.TensorP2PServer(t)
+    assert torch.equal(srv._CAPI_get_local_device_tensor(), t)
+    assert torch.equal(srv._CAPI_get_device_tensor(0), t.flatten())
+
+
+# ------------------------------------------------------------------ heat
+@pytest.mark.parametrize("bias", [False, True])
+def test_heat_matches_oracle(dgs, bias):
+    indptr, indices, probs = _hub_graph(2)
+    probs = probs + np.float32(0.05)
+    n = indptr.size - 1
+    heat = np.random.default_rng(1).random(n).astype(np.float32)
+    seeds = np.random.default_rng(2).permutation(n)[:150]
+    if bias:
+        got = dgs.ops._CAPI_compute_frontier_heat_with_bias(
+            _cuda(seeds), _cuda(indptr), _cuda(indices), _cuda(probs), _cuda(heat), 5, 0)
+    else:
+        got = dgs.ops._CAPI_compute_frontier_heat(_cuda(seeds), _cuda(indptr), _cuda(indices),
+                                                  _cuda(heat), 5, 0)
+    exp = O.frontier_heat(seeds, indptr, indices, heat, 5, probs=probs if bias else None)
+    np.testing.assert_allclose(got.cpu().numpy(), exp, rtol=1e-5, atol=1e-6)
+
+
+def test_heat_uva_host_graph(dgs):
+    indptr, indices, _ = _hub_graph(4)
+    n = indptr.size - 1
+    ip, ix = torch.from_numpy(indptr), torch.from_numpy(indices)
+    dgs.ops._CAPI_tensor_pin_memory(ip)
+    dgs.ops._CAPI_tensor_pin_memory(ix)
+    heat = torch.rand(n, device="cuda")
+    seeds = torch.arange(0, n, 3, device="cuda")
+    got = dgs.ops._CAPI_compute_frontier_heat(seeds, ip, ix, heat, 10, 0)
+    exp = O.frontier_heat(seeds.cpu().numpy(), indptr, indices, heat.cpu().numpy(), 10)
+    np.testing.assert_allclose(got.cpu().numpy(), exp, rtol=1e-5, atol=1e-6)
+    dgs.ops._CAPI_tensor_unpin_memory(ip)
+    dgs.ops._CAPI_tensor_unpin_memory(ix)
+
+
+# ------------------------------------------------------------------ larger graph
+def test_rmat_scale16_sampler_bit_exact(dgs):
+    from DistGNN.dataloading.synthetic import rmat_csc_numpy
+    indptr, indices = rmat_csc_numpy(16, 12, seed=20261015)
+    n = indptr.size - 1
+    sampler = dgs.classes.P2PCacheSampler(torch.from_numpy(indptr), torch.from_numpy(indices),
+                                          torch.Tensor(), torch.arange(n), 0)
+    seeds = np.random.default_rng(2).permutation(n)[:1024]
+    dgs.ops._CAPI_set_random_seed(99)
+    got = sampler._CAPI_sample_node_classifiction(_cuda(seeds), [15, 10, 5], False)
+    exp = O.node_classification_sample(seeds, indptr, indices, [15, 10, 5], False,
+                                       O.launch_seeds(99, 3))
+    for (gs, gf, gr, gc), (es, ef, er, ec) in zip(got, exp):
+        assert np.array_equal(gf.cpu().numpy(), ef)
+        assert np.array_equal(gr.cpu().numpy(), er)
+        assert np.array_equal(gc.cpu().numpy(), ec)
