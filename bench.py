@@ -1,0 +1,256 @@
+"""Benchmark of the DGS-AMD hot path (BASELINE.json metric: sampled edges/sec + feature-gather
+GB/s, fan-out [15,10,5]).
+
+One step = one training-loop data pass of the reference (example/graphsage/
+node_classification.py:219-229): P2PCacheSampler._CAPI_sample_node_classifiction(seeds,
+[15,10,5]) + P2PCacheFeatureServer._CAPI_get_feature(input nodes) +
+ops._CAPI_cuda_index_select(labels, seeds), on a synthetic products-like RMAT graph (configs[1]:
+uniform sampler + full-feature gather, d = 100, whole graph in HBM).  Inputs are resident in HBM
+before the timed region.  N > 1 (torchrun): every rank holds the graph (replicated, weak
+scaling) and samples its own slice of the train nids; no collective runs in the timed loop.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--scale S --ef E]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "dist-gnn_amd", "python"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=1024)
+    p.add_argument("--fan-out", type=str, default="15,10,5")
+    p.add_argument("--scale", type=int, default=21)   # products-like: 2,097,152 nodes
+    p.add_argument("--ef", type=int, default=59)      # 123.7 M edges
+    p.add_argument("--dim", type=int, default=100)
+    p.add_argument("--shard", action="store_true",
+                   help="cache node v on GPU v %% N (P2P over xGMI) instead of replicating")
+    p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--seed", type=int, default=20261015)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    import dgs
+    from DistGNN.dataloading import SeedGenerator
+    from DistGNN.dataloading.synthetic import rmat_csc_torch
+    if world > 1:
+        from DistGNN.dist import create_communicator
+        create_communicator(world)
+
+    fan_out = [int(x) for x in args.fan_out.split(",")]
+    dev = torch.device("cuda", local_rank)
+
+    # ---------------- synthetic inputs (identical on every rank)
+    t0 = time.time()
+    indptr_d, indices_d = rmat_csc_torch(args.scale, args.ef, seed=args.seed, device=dev)
+    N = indptr_d.numel() - 1
+    E = indices_d.numel()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(11)
+    feats_d = torch.randn(N, args.dim, generator=gen, device=dev)
+    labels_d = torch.randint(0, 47, (N,), generator=gen, device=dev)
+    indptr, indices = indptr_d.cpu(), indices_d.cpu()
+    feats, labels = feats_d.cpu(), labels_d.cpu()
+    del indptr_d, indices_d, feats_d, labels_d
+    torch.cuda.empty_cache()
+    g2 = torch.Generator()
+    g2.manual_seed(2)
+    train = torch.randperm(N, generator=g2)[: N // 10]
+    per = (train.numel() + world - 1) // world
+    train_local = train[rank * per:(rank + 1) * per].to(dev)
+    log(f"[bench] graph N={N} E={E} d={args.dim} built in {time.time() - t0:.1f}s")
+
+    # ---------------- services: whole graph + all features in HBM (configs[1])
+    if args.shard and world > 1:
+        cache = torch.arange(rank, N, world)
+    else:
+        cache = torch.arange(N)
+    t0 = time.time()
+    sampler = dgs.classes.P2PCacheSampler(indptr, indices, torch.Tensor(), cache, local_rank)
+    server = dgs.classes.P2PCacheFeatureServer(feats, cache, local_rank)
+    labels_dev = labels.to(dev)
+    torch.cuda.synchronize()
+    log(f"[bench] services ready in {time.time() - t0:.1f}s")
+    dgs.ops._CAPI_set_random_seed(args.seed + rank)
+
+    torch.manual_seed(1)
+    loader = iter(SeedGenerator(train_local, args.batch, shuffle=True, drop_last=True))
+
+    def next_seeds():
+        nonlocal loader
+        try:
+            return next(loader)
+        except StopIteration:
+            loader = iter(SeedGenerator(train_local, args.batch, shuffle=True, drop_last=True))
+            return next(loader)
+
+    def step():
+        seeds = next_seeds()
+        blocks = sampler._CAPI_sample_node_classifiction(seeds, fan_out, False)
+        x = server._CAPI_get_feature(blocks[-1][1])
+        y = dgs.ops._CAPI_cuda_index_select(labels_dev, seeds)
+        return sum(b[2].numel() for b in blocks), x.shape[0], x, y
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dgs.ops.profile_enable(True)
+    edges = rows = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        e, r, _, _ = step()
+        edges += e
+        rows += r
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    prof = dgs.ops.profile_read()
+    dgs.ops.profile_enable(False)
+
+    row_bytes = args.dim * 4
+    gather_bytes = rows * (2 * row_bytes + 8)  # read row + write row + read nid
+    if dist:
+        t = torch.tensor([elapsed, float(edges), float(rows), float(gather_bytes),
+                          prof["gather_ms"]], dtype=torch.float64, device=dev)
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed = float(mx[0])
+        edges_all, rows_all, gbytes_all = float(t[1]), float(t[2]), float(t[3])
+    else:
+        edges_all, rows_all, gbytes_all = float(edges), float(rows), float(gather_bytes)
+
+    # roofline of the dominant HBM kernel (feature gather), measured live with HIP events
+    g_ms = prof["gather_ms"] / max(prof["gather_launches"], 1)
+    g_bytes = gather_bytes / max(prof["gather_launches"], 1)
+    achieved = g_bytes / (g_ms * 1e-3) / 1e9 if g_ms > 0 else 0.0
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "gather_pmc.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get("dim") == args.dim:
+                traffic = pmc.get("hbm_bytes_per_row") * (rows / max(prof["gather_launches"], 1))
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(indptr, indices, feats, train, fan_out, args)
+
+    out = {
+        "metric": "sampled edges/sec + feature-gather GB/s, fan-out [15,10,5]",
+        "value": edges_all / elapsed,
+        "unit": "sampled edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (RMAT a,b,c,d=.57,.19,.19,.05; randn f32 features; no OGB offline)",
+        "config": {
+            "workload": (f"products-like RMAT scale {args.scale} ef {args.ef} (N={N}, E={E}), "
+                         f"uniform sampler fan-out {fan_out} without replacement, B={args.batch} "
+                         f"seeds/step/GPU, + full-feature gather d={args.dim} f32 + label gather; "
+                         + ("graph sharded v%N over GPUs (P2P)" if args.shard and world > 1
+                            else "whole graph + features in HBM on every GPU")),
+            "fan_out": fan_out, "batch_per_gpu": args.batch, "num_nodes": N, "num_edges": E,
+            "feat_dim": args.dim, "parallelism": f"dp{world} (seed-parallel)",
+        },
+        "gather_GBps": achieved,
+        "gather_GBps_wall": gbytes_all / elapsed / 1e9,
+        "sampled_edges_per_step": edges_all / args.steps,
+        "gathered_rows_per_step": rows_all / args.steps,
+        "sample_hops_ms_per_step": prof["sample_ms"] / args.steps,
+        "gather_kernel_ms_per_step": prof["gather_ms"] / args.steps,
+        "label_select_kernel_ms_per_step": prof["select_ms"] / args.steps,
+        "roofline": {
+            "bound": "hbm", "kernel": "k_gather<16, TableSrc> (P2PCacheFeatureServer gather)",
+            "timing": "hipExtLaunchKernelGGL start/stop events (GPU-side kernel start/end)",
+            "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS,
+            "bytes_per_launch": g_bytes, "avg_launch_ms": g_ms,
+            "traffic": traffic,
+        },
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(indptr, indices, feats, train, fan_out, args):
+    """The oracle's OpenMP restatement on the host cores (DGL is not installed): uniform
+    row-wise sampling per hop + relabel + feature gather, same graph and batch size."""
+    from oracle import oracle as O
+    threads = int(os.environ.get("DGS_CPU_THREADS", "16"))
+    ip, ix = indptr.numpy(), indices.numpy()
+    fx = feats.numpy()
+    rng = np.random.default_rng(1)
+    seeds_all = train.numpy()
+    edges = rows = batches = 0
+    t0 = time.perf_counter()
+    while True:
+        seeds = seeds_all[rng.integers(0, seeds_all.size, args.batch)]
+        cur = seeds
+        for h, k in enumerate(reversed(fan_out)):
+            r, c = O.sample_uniform(cur, ip, ix, k, False, 1000 + batches * 8 + h,
+                                    nthreads=threads)
+            uniq, (rr, cc) = O.relabel([cur, c], [r, c])
+            edges += c.size
+            cur = uniq
+        x = O.index_select(fx, cur, nthreads=threads)
+        rows += x.shape[0]
+        batches += 1
+        if time.perf_counter() - t0 > args.cpu_baseline_seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": edges / dt, "unit": "sampled edges/s", "cores": threads, "kind": "port",
+            "gather_GBps": rows * (2 * args.dim * 4 + 8) / dt / 1e9,
+            "sample": (f"{batches} batches of B={args.batch}, fan-out {fan_out}, same graph; "
+                       f"oracle/dgs_oracle.c OpenMP sampler ({threads} threads) + serial relabel "
+                       f"+ OpenMP gather, {dt:.1f}s")}
+
+
+if __name__ == "__main__":
+    main()

@@ -149,15 +149,17 @@ int dgs_sample_neighbors(const int64_t *seeds, int64_t Sn, const int64_t *indptr
     RowSrc src{};
     src.ntab = nullptr;
     src.indptr = dev_ptr(indptr, "indptr");
-    src.indices.p[0] = dev_ptr(indices, "indices");
+    src.indices = dev_ptr(indices, "indices");
+    src.indices_base.p[0] = src.indices;
     src.probs.p[0] = dev_ptr(probs, "probs");
     seeds = dev_ptr(seeds, "seeds");
     HopScratch &ws = op_scratch();
     int64_t *tmp = nullptr;  // [0] = nnz, then rowpos[S*k]
     const int64_t cap = Sn * num_picks;
     DGS_HIP(hipMallocAsync((void **)&tmp, sizeof(int64_t) * (size_t)(cap + 1), st));
-    sample_hop(src, seeds, Sn, num_picks, replace != 0, probs != nullptr, rng().next(), tmp + 1,
-               out_col, tmp, ws, st);
+    const Table no_table{nullptr, nullptr, nullptr, nullptr, 0};
+    sample_hop(src, seeds, Count{Sn, nullptr}, num_picks, replace != 0, probs != nullptr,
+               rng().next(), tmp + 1, out_col, tmp, no_table, ws, st);
     int64_t nnz = 0;
     DGS_HIP(hipMemcpyAsync(&nnz, tmp, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     DGS_HIP(hipStreamSynchronize(st));
@@ -350,7 +352,7 @@ int dgs_profile_enable(int on) {
 }
 
 int dgs_profile_read(double *gather_ms, int64_t *gather_launches, double *sample_ms,
-                     int64_t *sample_calls) {
+                     int64_t *sample_calls, double *select_ms, int64_t *select_launches) {
   return guard([&] {
     profile_collect();
     Profiler &p = profiler();
@@ -358,8 +360,10 @@ int dgs_profile_read(double *gather_ms, int64_t *gather_launches, double *sample
     *gather_launches = p.gather_n;
     *sample_ms = p.sample_ms;
     *sample_calls = p.sample_n;
-    p.gather_ms = p.sample_ms = 0;
-    p.gather_n = p.sample_n = 0;
+    if (select_ms) *select_ms = p.select_ms;
+    if (select_launches) *select_launches = p.select_n;
+    p.gather_ms = p.sample_ms = p.select_ms = 0;
+    p.gather_n = p.sample_n = p.select_n = 0;
   });
 }
 

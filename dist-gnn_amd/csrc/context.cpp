@@ -155,6 +155,15 @@ Profiler &profiler() {
   return p;
 }
 
+KernelEvents profile_kernel(int which) {
+  KernelEvents ev;
+  if (!profiler().on) return ev;
+  ev.start = take_event();
+  ev.stop = take_event();
+  pending().push_back(EvPair{ev.start, ev.stop, which});
+  return ev;
+}
+
 void profile_begin(hipStream_t st, int which) {
   if (!profiler().on) return;
   EvPair ev{take_event(), nullptr, which};
@@ -184,6 +193,9 @@ void profile_collect() {
     if (ev.which == 0) {
       profiler().gather_ms += ms;
       profiler().gather_n += 1;
+    } else if (ev.which == 2) {
+      profiler().select_ms += ms;
+      profiler().select_n += 1;
     } else {
       profiler().sample_ms += ms;
       profiler().sample_n += 1;

@@ -39,24 +39,25 @@ __global__ __launch_bounds__(256) void k_extract_rows(const int64_t *nids, int64
   }
 }
 
-__global__ void k_ntab_init_host(NodeEntry *ntab, const int64_t *indptr, int64_t n) {
+__global__ void k_ntab_init_host(NodeEntry *ntab, const int64_t *indptr, int64_t n,
+                                 const int64_t *indices) {
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v < n) {
     const int64_t b = indptr[v], e = indptr[v + 1];
     NodeEntry ne;
-    ne.off = b;
+    ne.ptr = indices + b;
     ne.dl = (e - b) | ((int64_t)kLocHost << kLocShift);
     ntab[v] = ne;
   }
 }
 
 __global__ void k_ntab_assign(NodeEntry *ntab, const int64_t *nids, const int64_t *sub_indptr,
-                              int64_t n, int64_t loc) {
+                              int64_t n, int64_t loc, const int64_t *sub_indices) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     const int64_t b = sub_indptr[i], e = sub_indptr[i + 1];
     NodeEntry ne;
-    ne.off = b;
+    ne.ptr = sub_indices + b;
     ne.dl = (e - b) | (loc << kLocShift);
     ntab[nids[i]] = ne;
   }
@@ -114,6 +115,16 @@ __global__ void k_cached_scatter(const int64_t *tab, int64_t n, const int64_t *p
   devid[p] = loc;
 }
 
+__global__ void k_loctab_init(int64_t *tab, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) tab[i] = ((int64_t)kLocHost << kLocShift) | i;
+}
+
+__global__ void k_loctab_assign(int64_t *tab, const int64_t *nids, int64_t n, int64_t loc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) tab[nids[i]] = (loc << kLocShift) | i;
+}
+
 __global__ void k_take_i64(const int64_t *src, const int64_t *idx, int64_t n, int64_t *out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = src[idx[i]];
@@ -162,18 +173,19 @@ void extract_edge_data(const int64_t *nids, int64_t n, const int64_t *indptr,
   DGS_LAUNCH_CHECK();
 }
 
-void ntab_init_host(NodeEntry *ntab, const int64_t *indptr, int64_t n, hipStream_t st) {
+void ntab_init_host(NodeEntry *ntab, const int64_t *indptr, int64_t n, const int64_t *indices,
+                    hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_ntab_init_host, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ntab,
-                     indptr, n);
+                     indptr, n, indices);
   DGS_LAUNCH_CHECK();
 }
 
 void ntab_assign(NodeEntry *ntab, const int64_t *nids, const int64_t *sub_indptr, int64_t n,
-                 int loc, hipStream_t st) {
+                 int loc, const int64_t *sub_indices, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_ntab_assign, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ntab,
-                     nids, sub_indptr, n, (int64_t)loc);
+                     nids, sub_indptr, n, (int64_t)loc, sub_indices);
   DGS_LAUNCH_CHECK();
 }
 
@@ -209,6 +221,19 @@ void cache_map_compact(const int64_t *tab, int64_t n, int64_t *key, int64_t *idx
   DGS_LAUNCH_CHECK();
   DGS_HIP(hipFreeAsync(scratch, st));
   DGS_HIP(hipFreeAsync(pos, st));
+}
+
+void loctab_init_host(int64_t *tab, int64_t n, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_loctab_init, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, tab, n);
+  DGS_LAUNCH_CHECK();
+}
+
+void loctab_assign(int64_t *tab, const int64_t *nids, int64_t n, int loc, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_loctab_assign, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, tab,
+                     nids, n, (int64_t)loc);
+  DGS_LAUNCH_CHECK();
 }
 
 void take_i64(const int64_t *src, const int64_t *idx, int64_t n, int64_t *out, hipStream_t st) {

@@ -100,16 +100,30 @@ struct PtrTable {
 };
 
 // Graph node table entry (16 B, one load per seed):
-//   off = offset of the node's first edge inside its location's edge arrays,
-//   dl  = degree | (location << 56).
+//   ptr = absolute (device-accessible) address of the node's first neighbour id in whichever
+//         location holds its row (local HBM cache, a peer's IPC-mapped cache, mapped host),
+//   dl  = degree | (location << 56)  (the location only selects the probs array).
 struct NodeEntry {
-  int64_t off;
+  const int64_t *ptr;
   int64_t dl;
+};
+
+// A count that is either known on the host (p == nullptr) or produced on the device by an
+// earlier kernel of the same stream (then `v` is only an upper bound used to size grids and
+// buffers).  Lets a whole multi-hop sample run without host synchronisation.
+struct Count {
+  int64_t v;
+  const int64_t *p;
+#ifdef __HIPCC__
+  __device__ __forceinline__ int64_t get() const { return p ? *p : v; }
+#endif
 };
 
 // ---------------------------------------------------------------------------------
 // Device helpers
 #ifdef __HIPCC__
+// Philox4x32-10 (curand / Random123 layout).  Each 32x32 product is one 64-bit multiply
+// (v_mad_u64_u32) instead of a mul_lo + mul_hi pair.
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -117,11 +131,19 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
       k.x += 0x9E3779B9u;
       k.y += 0xBB67AE85u;
     }
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
-    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k.x, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k.y,
+                   (uint32_t)p0);
   }
   return c;
+}
+
+// Wave-uniform 64-bit value -> scalar registers.
+__device__ __forceinline__ uint64_t wave_uniform(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ uint32_t u4_get(const uint4 &v, int w) {

@@ -2,6 +2,7 @@
 #pragma once
 
 #include "dgs_common.h"
+#include "dgs_table.cuh"
 
 namespace dgs {
 
@@ -9,14 +10,15 @@ namespace dgs {
 // out[i, :] = data[nid[i], :], a row_bytes byte copy per row.
 void gather_plain(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
                   int64_t n, void *out, hipStream_t st);
-// out[i, :] = row (ftab[nids[i]]) where ftab entries are (loc << 56) | row and loc indexes
-// `bases` (kLocHost = host array indexed by the nid itself).
-void gather_table(const int64_t *ftab, PtrTable bases, int64_t row_bytes, const int64_t *nids,
-                  int64_t n, void *out, hipStream_t st);
-// ftab[v] = (kLocHost << 56) | v for v < n
-void ftab_init_host(int64_t *ftab, int64_t n, hipStream_t st);
-// ftab[nids[i]] = (loc << 56) | i
-void ftab_assign(int64_t *ftab, const int64_t *nids, int64_t n, int loc, hipStream_t st);
+// out[i, :] = *(row_bytes at ftab[nids[i]]): ftab holds the absolute (device-accessible)
+// address of every node's feature row.  align_or = OR of all row base addresses.
+void gather_table(const int64_t *ftab, uintptr_t align_or, int64_t row_bytes,
+                  const int64_t *nids, int64_t n, void *out, hipStream_t st);
+// ftab[v] = base + v * row_bytes for v < n
+void ftab_init(int64_t *ftab, int64_t n, const void *base, int64_t row_bytes, hipStream_t st);
+// ftab[nids[i]] = base + i * row_bytes
+void ftab_assign(int64_t *ftab, const int64_t *nids, int64_t n, const void *base,
+                 int64_t row_bytes, hipStream_t st);
 
 // ---------------------------------------------------------------- CSR utilities (csr.hip)
 // sub_indptr[i] = sum_{j<i} deg(nids[j]), i = 0..n
@@ -25,11 +27,12 @@ void extract_indptr(const int64_t *nids, int64_t n, const int64_t *indptr, int64
 void extract_edge_data(const int64_t *nids, int64_t n, const int64_t *indptr,
                        const int64_t *sub_indptr, const void *edge_data, int64_t elem_bytes,
                        void *sub, hipStream_t st);
-// node table: ntab[v] = {indptr[v], deg(v) | host}
-void ntab_init_host(NodeEntry *ntab, const int64_t *indptr, int64_t n, hipStream_t st);
-// ntab[nids[i]] = {sub_indptr[i], (sub_indptr[i+1]-sub_indptr[i]) | loc<<56}
+// node table: ntab[v] = {indices + indptr[v], deg(v) | host << 56}
+void ntab_init_host(NodeEntry *ntab, const int64_t *indptr, int64_t n, const int64_t *indices,
+                    hipStream_t st);
+// ntab[nids[i]] = {sub_indices + sub_indptr[i], (sub_indptr[i+1]-sub_indptr[i]) | loc << 56}
 void ntab_assign(NodeEntry *ntab, const int64_t *nids, const int64_t *sub_indptr, int64_t n,
-                 int loc, hipStream_t st);
+                 int loc, const int64_t *sub_indices, hipStream_t st);
 // Compacts a (loc << 56 | row) table into (nid, row, loc) triples for every node whose
 // location is a GPU; *d_count receives the count.  key/idx/devid may be null (count only).
 void cache_map_compact(const int64_t *tab, int64_t n, int64_t *key, int64_t *idx,
@@ -47,33 +50,42 @@ void scan_exclusive(const int64_t *in, int64_t n, int64_t *out, void *scratch, h
 
 // ---------------------------------------------------------------- sampling (sample.hip)
 struct RowSrc {
-  // Node lookup: either a node table (graph shard context) or a plain CSR indptr.
-  const NodeEntry *ntab;  // if non-null
-  const int64_t *indptr;  // else
-  PtrTable indices;       // per-location edge arrays (indices)
-  PtrTable probs;         // per-location probabilities (biased) or all null
+  // Node lookup: either a node table (graph shard context) or a plain CSR indptr/indices.
+  const NodeEntry *ntab;   // if non-null
+  const int64_t *indptr;   // else (location 0)
+  const int64_t *indices;  // plain-CSR neighbour ids
+  PtrTable indices_base;   // per-location neighbour-id arrays (to locate probs)
+  PtrTable probs;          // per-location probabilities (biased) or all null
 };
 
 struct HopScratch {
-  DevBuf rowinfo, bsum, boff, hub, hubslot, rowpos, slot_of, tkey, tval, tlab, misc, cdf;
+  DevBuf rowinfo, tpre, bsum, boff, hub, hubcount, hubslot, rowpos, slot_of, tkey, tval, tlab,
+      misc, cdf;
   HostPinned host;
   uint64_t table_cap = 0;  // capacity currently allocated and clean
   bool table_dirty = false;
 };
 
-// One sampling hop over `seeds[S]` (device):
+// One sampling hop over `seeds[S]` (device; S may be a device-side count, then S.v bounds it):
 //   writes rowpos[e] (index of the seed row of edge e) and col[e] (neighbour nid),
-//   d_nnz receives nnz (device).  Capacities: S * k.
-void sample_hop(const RowSrc &src, const int64_t *seeds, int64_t S, int64_t k, bool replace,
+//   d_nnz receives nnz (device).  Capacities: S.v * k.
+// When `table.key` is set, every seed i and sampled neighbour (position S + e) is inserted
+// into the relabel table by the kernels that produce them.
+void sample_hop(const RowSrc &src, const int64_t *seeds, Count S, int64_t k, bool replace,
                 bool bias, uint64_t launch_seed, int64_t *rowpos, int64_t *col, int64_t *d_nnz,
-                HopScratch &ws, hipStream_t st);
+                const Table &table, HopScratch &ws, hipStream_t st);
+
+// Clean relabel table with capacity for n_ub insertions (marks the scratch dirty until the
+// hop's relabel pass has returned the touched slots to empty).
+Table relabel_table(HopScratch &ws, int64_t n_ub, hipStream_t st);
 
 // Relabel for the node-classification hop: mapping = cat(seeds[S], col[nnz]) where nnz is
 // read from d_nnz (device); writes unique ids to `unique` (first-occurrence order),
 // relabeled rows/cols to out_row/out_col (col may alias out_col), U to d_nunique.
-void relabel_hop(const int64_t *seeds, int64_t S, const int64_t *col, const int64_t *d_nnz,
-                 int64_t nnz_cap, const int64_t *rowpos, int64_t *unique, int64_t *out_row,
-                 int64_t *out_col, int64_t *d_nunique, HopScratch &ws, hipStream_t st);
+void relabel_hop(const int64_t *seeds, Count S, const int64_t *col, const int64_t *d_nnz,
+                 int64_t nnz_cap, const int64_t *rowpos, const Table &table, int64_t *unique,
+                 int64_t *out_row, int64_t *out_col, int64_t *d_nunique, HopScratch &ws,
+                 hipStream_t st);
 
 // Generic relabel (TensorRelabelCUDA): mapping[nm], req[nr] -> unique, relabeled req (-1 if
 // absent), d_nunique.
@@ -87,14 +99,24 @@ void take_i64(const int64_t *src, const int64_t *idx, int64_t n, int64_t *out, h
 // ---------------------------------------------------------------- profiling
 struct Profiler {
   bool on = false;
-  double gather_ms = 0, sample_ms = 0;
-  int64_t gather_n = 0, sample_n = 0;
+  double gather_ms = 0, sample_ms = 0, select_ms = 0;
+  int64_t gather_n = 0, sample_n = 0, select_n = 0;
 };
 Profiler &profiler();
-// Records begin/end events around `fn` on `st` when profiling is on; the elapsed time is
-// collected lazily by profile_collect().
+// which: 0 = feature-server gather kernel, 1 = sampling hop (events around the hop's
+// kernels), 2 = plain index_select gather kernel.
+// Kernel events: when profiling is on, returns (start, stop) events that hipExtLaunchKernelGGL
+// records at the kernel's own start / end; otherwise (null, null).
+struct KernelEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+KernelEvents profile_kernel(int which);
+// Stream events around a group of launches (wall time of the group on the stream).
 void profile_begin(hipStream_t st, int which);
 void profile_end(hipStream_t st, int which);
 void profile_collect();
+// cache-map helpers: tab[v] = (loc << 56) | row
+void loctab_init_host(int64_t *tab, int64_t n, hipStream_t st);
+void loctab_assign(int64_t *tab, const int64_t *nids, int64_t n, int loc, hipStream_t st);
 
 }  // namespace dgs

@@ -1,0 +1,66 @@
+// dgs_table.cuh -- the relabel hash table shared by the sampling kernels (which insert the
+// hop's seeds and sampled neighbours as they produce them) and relabel.hip (which ranks the
+// first occurrences and rewrites the COO).  Reference semantics: tensor_relabel.cu:17-29.
+#pragma once
+
+#include "dgs_common.h"
+
+namespace dgs {
+
+constexpr int64_t kTableEmpty = -1;
+constexpr int32_t kTableNoPos = 0x7FFFFFFF;
+
+struct Table {
+  int64_t *key;   // nullptr: no table (standalone sampling op)
+  int32_t *val;   // minimum position (first occurrence)
+  int32_t *lab;   // label = rank among first occurrences
+  uint32_t *slot_of;  // slot of every inserted position
+  uint64_t mask;
+};
+
+#ifdef __HIPCC__
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdULL;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ULL;
+  k ^= k >> 33;
+  return k;
+}
+
+// Inserts key x seen at position pos; the slot keeps min(pos).  64-bit CAS on the key, linear
+// probing, load factor <= 0.5.
+__device__ __forceinline__ uint32_t table_insert(const Table &t, int64_t x, int32_t pos) {
+  uint64_t h = fmix64((uint64_t)x) & t.mask;
+  while (true) {
+    int64_t cur = t.key[h];
+    if (cur == kTableEmpty) {
+      cur = (int64_t)atomicCAS((unsigned long long *)(t.key + h),
+                               (unsigned long long)kTableEmpty, (unsigned long long)x);
+      if (cur == kTableEmpty) cur = x;
+    }
+    if (cur == x) break;
+    h = (h + 1) & t.mask;
+  }
+  // val only decreases: skip the atomic when an earlier occurrence is already recorded
+  // (hub nodes recur thousands of times per hop; this removes the same-address atomics).
+  if (t.val[h] > pos) atomicMin(t.val + h, pos);
+  return (uint32_t)h;
+}
+
+__device__ __forceinline__ void table_record(const Table &t, int64_t x, int64_t pos) {
+  if (t.key) t.slot_of[pos] = table_insert(t, x, (int32_t)pos);
+}
+
+__device__ __forceinline__ int64_t table_find(const Table &t, int64_t x) {
+  uint64_t h = fmix64((uint64_t)x) & t.mask;
+  while (true) {
+    const int64_t cur = t.key[h];
+    if (cur == x) return (int64_t)h;
+    if (cur == kTableEmpty) return -1;
+    h = (h + 1) & t.mask;
+  }
+}
+#endif
+
+}  // namespace dgs

@@ -11,21 +11,41 @@
 // flight before its stores.  For the feature server the node -> (location, row) lookup is
 // fused into the same kernel (one 8-byte table load per row instead of a hash probe chain
 // plus a second pass).
+#include <hip/hip_ext.h>
+
 #include "dgs_common.h"
 #include "dgs_ops.h"
 
 namespace dgs {
 namespace {
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 template <int V>
 struct VecT;
+// Global-address-space pointer: row addresses come from memory, so without this the
+// compiler emits flat loads (counted on both vmcnt and lgkmcnt).
+template <typename T>
+using gptr = const __attribute__((address_space(1))) T *;
+template <typename T>
+__device__ __forceinline__ gptr<T> to_global(const void *p) {
+  return (gptr<T>)(uintptr_t)p;
+}
+
+// Pins a loaded value in registers at this point: keeps the compiler from sinking the load
+// into the (conditional) store branch, which would serialise the unrolled chunks again.
+__device__ __forceinline__ void keep(const u32x4 &v) { asm volatile("" ::"v"(v)); }
+__device__ __forceinline__ void keep(const u32x2 &v) { asm volatile("" ::"v"(v)); }
+__device__ __forceinline__ void keep(uint32_t v) { asm volatile("" ::"v"(v)); }
+__device__ __forceinline__ void keep(uint16_t v) { asm volatile("" ::"v"((uint32_t)v)); }
+__device__ __forceinline__ void keep(uint8_t v) { asm volatile("" ::"v"((uint32_t)v)); }
 template <>
 struct VecT<16> {
-  using T = uint4;
+  using T = u32x4;
 };
 template <>
 struct VecT<8> {
-  using T = uint2;
+  using T = u32x2;
 };
 template <>
 struct VecT<4> {
@@ -57,29 +77,31 @@ struct FastDivU32 {
   }
 };
 
+// Row sources.  row_ptr(r) = address of output row r's source row.  Each is split in two
+// stages (id load, then address) so the kernel can batch the loads of its U chunks.
 template <typename IdT>
 struct PlainSrc {
   const char *data;
   const IdT *nid;
   int64_t row_bytes;
   int64_t row_base;
-  __device__ __forceinline__ const char *row(uint32_t r) const {
-    return data + (int64_t)nid[row_base + r] * row_bytes;
-  }
+  using Key = int64_t;
+  __device__ __forceinline__ Key key(uint32_t r) const { return (int64_t)nid[row_base + r]; }
+  __device__ __forceinline__ const char *addr(Key k) const { return data + k * row_bytes; }
 };
 
+// Feature-server source: ftab[nid] holds the absolute address of the node's row (local HBM
+// cache, a peer GPU's IPC-mapped cache, or mapped host memory), so the fused lookup is one
+// 8-byte load per row with no per-location base indexing.
 struct TableSrc {
   const int64_t *ftab;
   const int64_t *nid;
-  PtrTable bases;
-  int64_t row_bytes;
+  int64_t row_bytes;  // unused (kept for a uniform launcher)
   int64_t row_base;
-  __device__ __forceinline__ const char *row(uint32_t r) const {
-    const int64_t v = nid[row_base + r];
-    const int64_t e = ftab[v];
-    const int loc = (int)((uint64_t)e >> kLocShift);
-    const int64_t idx = e & kOffMask;
-    return reinterpret_cast<const char *>(bases.p[loc]) + idx * row_bytes;
+  using Key = int64_t;
+  __device__ __forceinline__ Key key(uint32_t r) const { return nid[row_base + r]; }
+  __device__ __forceinline__ const char *addr(Key k) const {
+    return reinterpret_cast<const char *>(to_global<int64_t>(ftab)[k]);
   }
 };
 
@@ -92,16 +114,28 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nch
                                                            char *__restrict__ out) {
   using T = typename VecT<V>::T;
   const uint32_t base = blockIdx.x * (uint32_t)(kGatherThreads * kGatherUnroll) + threadIdx.x;
+  // Branch-free: out-of-range chunks re-read the last chunk and skip only the store, so the
+  // U independent id -> address -> row load chains issue back to back (3 waits, not 3U).
+  uint32_t r[kGatherUnroll], c[kGatherUnroll];
+  typename Src::Key key[kGatherUnroll];
+  const char *a[kGatherUnroll];
   T v[kGatherUnroll];
 #pragma unroll
   for (int u = 0; u < kGatherUnroll; ++u) {
-    const uint32_t g = base + u * kGatherThreads;
-    if (g < nchunks) {
-      const uint32_t r = fd.div(g);
-      const uint32_t c = g - r * cpr;
-      v[u] = *reinterpret_cast<const T *>(src.row(r) + (size_t)c * V);
-    }
+    uint32_t g = base + u * kGatherThreads;
+    g = g < nchunks ? g : nchunks - 1;
+    r[u] = fd.div(g);
+    c[u] = g - r[u] * cpr;
   }
+#pragma unroll
+  for (int u = 0; u < kGatherUnroll; ++u) key[u] = src.key(r[u]);
+#pragma unroll
+  for (int u = 0; u < kGatherUnroll; ++u) a[u] = src.addr(key[u]);
+#pragma unroll
+  for (int u = 0; u < kGatherUnroll; ++u)
+    v[u] = *to_global<T>(a[u] + (size_t)c[u] * V);
+#pragma unroll
+  for (int u = 0; u < kGatherUnroll; ++u) keep(v[u]);
 #pragma unroll
   for (int u = 0; u < kGatherUnroll; ++u) {
     const uint32_t g = base + u * kGatherThreads;
@@ -110,7 +144,8 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nch
 }
 
 template <typename Src>
-void launch_gather_v(int V, Src src, int64_t n, int64_t row_bytes, char *out, hipStream_t st) {
+void launch_gather_v(int V, Src src, int64_t n, int64_t row_bytes, char *out, hipStream_t st,
+                     int which) {
   const int64_t cpr = row_bytes / V;
   DGS_CHECK(cpr > 0 && cpr < (int64_t(1) << 30), "gather: unsupported row size");
   const int64_t max_rows = ((int64_t(1) << 31) - kGatherThreads * kGatherUnroll) / cpr;
@@ -122,12 +157,15 @@ void launch_gather_v(int V, Src src, int64_t n, int64_t row_bytes, char *out, hi
     const uint32_t nchunks = (uint32_t)(rows * cpr);
     const dim3 grid((unsigned)ceil_div(nchunks, kGatherThreads * kGatherUnroll));
     char *o = out + r0 * row_bytes;
+    const KernelEvents ev = profile_kernel(which);
+    const dim3 block(kGatherThreads);
+    const uint32_t c32 = (uint32_t)cpr;
     switch (V) {
-      case 16: hipLaunchKernelGGL((k_gather<16, Src>), grid, dim3(kGatherThreads), 0, st, s, nchunks, (uint32_t)cpr, fd, o); break;
-      case 8: hipLaunchKernelGGL((k_gather<8, Src>), grid, dim3(kGatherThreads), 0, st, s, nchunks, (uint32_t)cpr, fd, o); break;
-      case 4: hipLaunchKernelGGL((k_gather<4, Src>), grid, dim3(kGatherThreads), 0, st, s, nchunks, (uint32_t)cpr, fd, o); break;
-      case 2: hipLaunchKernelGGL((k_gather<2, Src>), grid, dim3(kGatherThreads), 0, st, s, nchunks, (uint32_t)cpr, fd, o); break;
-      default: hipLaunchKernelGGL((k_gather<1, Src>), grid, dim3(kGatherThreads), 0, st, s, nchunks, (uint32_t)cpr, fd, o); break;
+      case 16: hipExtLaunchKernelGGL((k_gather<16, Src>), grid, block, 0, st, ev.start, ev.stop, 0, s, nchunks, c32, fd, o); break;
+      case 8: hipExtLaunchKernelGGL((k_gather<8, Src>), grid, block, 0, st, ev.start, ev.stop, 0, s, nchunks, c32, fd, o); break;
+      case 4: hipExtLaunchKernelGGL((k_gather<4, Src>), grid, block, 0, st, ev.start, ev.stop, 0, s, nchunks, c32, fd, o); break;
+      case 2: hipExtLaunchKernelGGL((k_gather<2, Src>), grid, block, 0, st, ev.start, ev.stop, 0, s, nchunks, c32, fd, o); break;
+      default: hipExtLaunchKernelGGL((k_gather<1, Src>), grid, block, 0, st, ev.start, ev.stop, 0, s, nchunks, c32, fd, o); break;
     }
     DGS_LAUNCH_CHECK();
   }
@@ -139,14 +177,15 @@ int pick_vec(int64_t row_bytes, uintptr_t align_or) {
   return 1;
 }
 
-__global__ void k_ftab_init_host(int64_t *ftab, int64_t n) {
+__global__ void k_ftab_init(int64_t *ftab, int64_t n, const char *base, int64_t row_bytes) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) ftab[i] = ((int64_t)kLocHost << kLocShift) | i;
+  if (i < n) ftab[i] = (int64_t)(base + i * row_bytes);
 }
 
-__global__ void k_ftab_assign(int64_t *ftab, const int64_t *nids, int64_t n, int64_t loc) {
+__global__ void k_ftab_assign(int64_t *ftab, const int64_t *nids, int64_t n, const char *base,
+                              int64_t row_bytes) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) ftab[nids[i]] = (loc << kLocShift) | i;
+  if (i < n) ftab[nids[i]] = (int64_t)(base + i * row_bytes);
 }
 
 }  // namespace
@@ -155,41 +194,36 @@ void gather_plain(const void *data, int64_t row_bytes, const void *nid, int nid_
                   int64_t n, void *out, hipStream_t st) {
   if (n <= 0 || row_bytes <= 0) return;
   const int V = pick_vec(row_bytes, (uintptr_t)data | (uintptr_t)out);
-  profile_begin(st, 0);
   if (nid_bytes == 8) {
     PlainSrc<int64_t> s{(const char *)data, (const int64_t *)nid, row_bytes, 0};
-    launch_gather_v(V, s, n, row_bytes, (char *)out, st);
+    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 2);
   } else {
     DGS_CHECK(nid_bytes == 4, "index ids must be int32 or int64");
     PlainSrc<int32_t> s{(const char *)data, (const int32_t *)nid, row_bytes, 0};
-    launch_gather_v(V, s, n, row_bytes, (char *)out, st);
+    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 2);
   }
-  profile_end(st, 0);
 }
 
-void gather_table(const int64_t *ftab, PtrTable bases, int64_t row_bytes, const int64_t *nids,
-                  int64_t n, void *out, hipStream_t st) {
+void gather_table(const int64_t *ftab, uintptr_t align_or, int64_t row_bytes,
+                  const int64_t *nids, int64_t n, void *out, hipStream_t st) {
   if (n <= 0 || row_bytes <= 0) return;
-  uintptr_t a = (uintptr_t)out;
-  for (int i = 0; i <= kMaxDevices; ++i) a |= (uintptr_t)bases.p[i];
-  const int V = pick_vec(row_bytes, a);
-  TableSrc s{ftab, nids, bases, row_bytes, 0};
-  profile_begin(st, 0);
-  launch_gather_v(V, s, n, row_bytes, (char *)out, st);
-  profile_end(st, 0);
+  const int V = pick_vec(row_bytes, align_or | (uintptr_t)out);
+  TableSrc s{ftab, nids, row_bytes, 0};
+  launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0);
 }
 
-void ftab_init_host(int64_t *ftab, int64_t n, hipStream_t st) {
+void ftab_init(int64_t *ftab, int64_t n, const void *base, int64_t row_bytes, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_ftab_init_host, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ftab,
-                     n);
+  hipLaunchKernelGGL(k_ftab_init, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ftab, n,
+                     (const char *)base, row_bytes);
   DGS_LAUNCH_CHECK();
 }
 
-void ftab_assign(int64_t *ftab, const int64_t *nids, int64_t n, int loc, hipStream_t st) {
+void ftab_assign(int64_t *ftab, const int64_t *nids, int64_t n, const void *base,
+                 int64_t row_bytes, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_ftab_assign, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ftab,
-                     nids, n, (int64_t)loc);
+                     nids, n, (const char *)base, row_bytes);
   DGS_LAUNCH_CHECK();
 }
 

@@ -12,55 +12,14 @@
 // the relabel pass itself (only the slots this hop touched), so no per-hop memset.
 #include "dgs_block.cuh"
 #include "dgs_ops.h"
+#include "dgs_table.cuh"
 
 namespace dgs {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int64_t kEmpty = -1;
-constexpr int32_t kNoPos = 0x7FFFFFFF;
-
-__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
-  k ^= k >> 33;
-  k *= 0xff51afd7ed558ccdULL;
-  k ^= k >> 33;
-  k *= 0xc4ceb9fe1a85ec53ULL;
-  k ^= k >> 33;
-  return k;
-}
-
-struct Table {
-  int64_t *key;
-  int32_t *val;  // minimum position (first occurrence)
-  int32_t *lab;  // label = rank among first occurrences
-  uint64_t mask;
-};
-
-__device__ __forceinline__ uint32_t table_insert(const Table &t, int64_t x, int32_t pos) {
-  uint64_t h = fmix64((uint64_t)x) & t.mask;
-  while (true) {
-    int64_t cur = t.key[h];
-    if (cur == kEmpty) {
-      cur = (int64_t)atomicCAS((unsigned long long *)(t.key + h), (unsigned long long)kEmpty,
-                               (unsigned long long)x);
-      if (cur == kEmpty) cur = x;
-    }
-    if (cur == x) break;
-    h = (h + 1) & t.mask;
-  }
-  atomicMin(t.val + h, pos);
-  return (uint32_t)h;
-}
-
-__device__ __forceinline__ int64_t table_find(const Table &t, int64_t x) {
-  uint64_t h = fmix64((uint64_t)x) & t.mask;
-  while (true) {
-    const int64_t cur = t.key[h];
-    if (cur == x) return (int64_t)h;
-    if (cur == kEmpty) return -1;
-    h = (h + 1) & t.mask;
-  }
-}
+constexpr int64_t kEmpty = kTableEmpty;
+constexpr int32_t kNoPos = kTableNoPos;
 
 // element i of cat(a[na], b[*nb_ptr])
 __device__ __forceinline__ int64_t elem(const int64_t *a, int64_t na, const int64_t *b,
@@ -68,34 +27,35 @@ __device__ __forceinline__ int64_t elem(const int64_t *a, int64_t na, const int6
   return i < na ? a[i] : b[i - na];
 }
 
-__global__ __launch_bounds__(kThreads) void k_insert(const int64_t *a, int64_t na,
+__global__ __launch_bounds__(kThreads) void k_insert(const int64_t *a, Count nac,
                                                      const int64_t *b, const int64_t *d_nb,
-                                                     int64_t nb_fixed, Table t,
-                                                     uint32_t *slot_of) {
+                                                     int64_t nb_fixed, Table t) {
+  const int64_t na = nac.get();
   const int64_t n = na + (d_nb ? *d_nb : nb_fixed);
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
-  slot_of[i] = table_insert(t, elem(a, na, b, i), (int32_t)i);
+  t.slot_of[i] = table_insert(t, elem(a, na, b, i), (int32_t)i);
 }
 
-__global__ __launch_bounds__(kThreads) void k_flag_count(int64_t na, const int64_t *d_nb,
+__global__ __launch_bounds__(kThreads) void k_flag_count(Count nac, const int64_t *d_nb,
                                                          int64_t nb_fixed, Table t,
                                                          const uint32_t *slot_of, int64_t *bcnt) {
   __shared__ int64_t lds[kThreads / 64];
-  const int64_t n = na + (d_nb ? *d_nb : nb_fixed);
+  const int64_t n = nac.get() + (d_nb ? *d_nb : nb_fixed);
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   const int64_t f = (i < n && t.val[slot_of[i]] == (int32_t)i) ? 1 : 0;
   const int64_t s = block_sum<kThreads>(f, lds);
   if (threadIdx.x == 0) bcnt[blockIdx.x] = s;
 }
 
-__global__ __launch_bounds__(kThreads) void k_scatter(const int64_t *a, int64_t na,
+__global__ __launch_bounds__(kThreads) void k_scatter(const int64_t *a, Count nac,
                                                       const int64_t *b, const int64_t *d_nb,
                                                       int64_t nb_fixed, Table t,
                                                       const uint32_t *slot_of,
                                                       const int64_t *boff, int64_t nblocks,
                                                       int64_t *unique, int64_t *d_nunique) {
   __shared__ int64_t lds[kThreads / 64];
+  const int64_t na = nac.get();
   const int64_t n = na + (d_nb ? *d_nb : nb_fixed);
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   uint32_t sl = 0;
@@ -116,10 +76,11 @@ __global__ __launch_bounds__(kThreads) void k_scatter(const int64_t *a, int64_t 
 
 // Hop relabel: out_col[e] = lab(slot_of[na + e]), out_row[e] = lab(slot_of[rowpos[e]]);
 // then the touched slots are returned to empty.
-__global__ __launch_bounds__(kThreads) void k_relabel_hop(int64_t na, const int64_t *d_nb,
+__global__ __launch_bounds__(kThreads) void k_relabel_hop(Count nac, const int64_t *d_nb,
                                                           Table t, const uint32_t *slot_of,
                                                           const int64_t *rowpos,
                                                           int64_t *out_row, int64_t *out_col) {
+  const int64_t na = nac.get();
   const int64_t nb = *d_nb;
   const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (e < nb) {
@@ -162,8 +123,11 @@ __global__ void k_table_init(int64_t *key, int32_t *val, uint64_t cap) {
   }
 }
 
-// Make sure the persistent table has a clean region of at least `need` slots.
-Table prepare_table(HopScratch &ws, int64_t n_ub, hipStream_t st) {
+}  // namespace
+
+// Makes sure the persistent table has a clean region of at least 2 * n_ub slots.
+Table relabel_table(HopScratch &ws, int64_t n_ub, hipStream_t st) {
+  DGS_CHECK(n_ub < (int64_t(1) << 31), "relabel input too large");
   const uint64_t cap = next_pow2((uint64_t)(2 * (n_ub > 0 ? n_ub : 1)));
   DGS_CHECK(cap <= (uint64_t(1) << 32), "relabel table too large");
   if (cap > ws.table_cap || ws.table_dirty) {
@@ -177,38 +141,32 @@ Table prepare_table(HopScratch &ws, int64_t n_ub, hipStream_t st) {
     ws.table_cap = alloc;
     ws.table_dirty = false;
   }
-  Table t{ws.tkey.as<int64_t>(), ws.tval.as<int32_t>(), ws.tlab.as<int32_t>(), cap - 1};
-  return t;
+  ws.slot_of.ensure(sizeof(uint32_t) * (size_t)(n_ub > 0 ? n_ub : 1));
+  return Table{ws.tkey.as<int64_t>(), ws.tval.as<int32_t>(), ws.tlab.as<int32_t>(),
+               ws.slot_of.as<uint32_t>(), cap - 1};
 }
 
-}  // namespace
-
-void relabel_hop(const int64_t *seeds, int64_t S, const int64_t *col, const int64_t *d_nnz,
-                 int64_t nnz_cap, const int64_t *rowpos, int64_t *unique, int64_t *out_row,
-                 int64_t *out_col, int64_t *d_nunique, HopScratch &ws, hipStream_t st) {
-  const int64_t n_ub = S + nnz_cap;
-  DGS_CHECK(n_ub < (int64_t(1) << 31), "relabel input too large");
-  ws.table_dirty = true;  // until the clean-up pass is enqueued
-  Table t = prepare_table(ws, n_ub, st);
-  ws.table_dirty = true;
+// The hop's seeds and sampled neighbours were already inserted by the sampling kernels
+// (sample_hop with this Table); what is left is ranking the first occurrences and the COO
+// rewrite.
+void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64_t *d_nnz,
+                 int64_t nnz_cap, const int64_t *rowpos, const Table &t, int64_t *unique,
+                 int64_t *out_row, int64_t *out_col, int64_t *d_nunique, HopScratch &ws,
+                 hipStream_t st) {
+  const int64_t n_ub = Sc.v + nnz_cap;
   const int64_t nblk = ceil_div(n_ub > 0 ? n_ub : 1, kThreads);
-  ws.slot_of.ensure(sizeof(uint32_t) * (size_t)(n_ub > 0 ? n_ub : 1));
   ws.misc.ensure(sizeof(int64_t) * (size_t)(2 * nblk + 2));
-  uint32_t *slot_of = ws.slot_of.as<uint32_t>();
   int64_t *bcnt = ws.misc.as<int64_t>();
   int64_t *boff = bcnt + nblk;
-  hipLaunchKernelGGL(k_insert, dim3((unsigned)nblk), dim3(kThreads), 0, st, seeds, S, col,
-                     d_nnz, (int64_t)0, t, slot_of);
-  DGS_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_flag_count, dim3((unsigned)nblk), dim3(kThreads), 0, st, S, d_nnz,
-                     (int64_t)0, t, slot_of, bcnt);
+  hipLaunchKernelGGL(k_flag_count, dim3((unsigned)nblk), dim3(kThreads), 0, st, Sc, d_nnz,
+                     (int64_t)0, t, t.slot_of, bcnt);
   DGS_LAUNCH_CHECK();
   scan_small(bcnt, nblk, boff, st);
-  hipLaunchKernelGGL(k_scatter, dim3((unsigned)nblk), dim3(kThreads), 0, st, seeds, S, col,
-                     d_nnz, (int64_t)0, t, slot_of, boff, nblk, unique, d_nunique);
+  hipLaunchKernelGGL(k_scatter, dim3((unsigned)nblk), dim3(kThreads), 0, st, seeds, Sc, col,
+                     d_nnz, (int64_t)0, t, t.slot_of, boff, nblk, unique, d_nunique);
   DGS_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_relabel_hop, dim3((unsigned)nblk), dim3(kThreads), 0, st, S, d_nnz, t,
-                     slot_of, rowpos, out_row, out_col);
+  hipLaunchKernelGGL(k_relabel_hop, dim3((unsigned)nblk), dim3(kThreads), 0, st, Sc, d_nnz, t,
+                     t.slot_of, rowpos, out_row, out_col);
   DGS_LAUNCH_CHECK();
   ws.table_dirty = false;
 }
@@ -216,25 +174,22 @@ void relabel_hop(const int64_t *seeds, int64_t S, const int64_t *col, const int6
 void relabel_generic(const int64_t *mapping, int64_t nm, const int64_t *req, int64_t nr,
                      int64_t *unique, int64_t *req_out, int64_t *d_nunique, HopScratch &ws,
                      hipStream_t st) {
-  DGS_CHECK(nm < (int64_t(1) << 31), "relabel input too large");
-  ws.table_dirty = true;
-  Table t = prepare_table(ws, nm, st);
+  Table t = relabel_table(ws, nm, st);
   ws.table_dirty = true;
   const int64_t nblk = ceil_div(nm > 0 ? nm : 1, kThreads);
-  ws.slot_of.ensure(sizeof(uint32_t) * (size_t)(nm > 0 ? nm : 1));
   ws.misc.ensure(sizeof(int64_t) * (size_t)(2 * nblk + 2));
-  uint32_t *slot_of = ws.slot_of.as<uint32_t>();
   int64_t *bcnt = ws.misc.as<int64_t>();
   int64_t *boff = bcnt + nblk;
-  hipLaunchKernelGGL(k_insert, dim3((unsigned)nblk), dim3(kThreads), 0, st, mapping, nm,
-                     (const int64_t *)nullptr, (const int64_t *)nullptr, (int64_t)0, t, slot_of);
+  const Count nmc{nm, nullptr};
+  hipLaunchKernelGGL(k_insert, dim3((unsigned)nblk), dim3(kThreads), 0, st, mapping, nmc,
+                     (const int64_t *)nullptr, (const int64_t *)nullptr, (int64_t)0, t);
   DGS_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_flag_count, dim3((unsigned)nblk), dim3(kThreads), 0, st, nm,
-                     (const int64_t *)nullptr, (int64_t)0, t, slot_of, bcnt);
+  hipLaunchKernelGGL(k_flag_count, dim3((unsigned)nblk), dim3(kThreads), 0, st, nmc,
+                     (const int64_t *)nullptr, (int64_t)0, t, t.slot_of, bcnt);
   DGS_LAUNCH_CHECK();
   scan_small(bcnt, nblk, boff, st);
-  hipLaunchKernelGGL(k_scatter, dim3((unsigned)nblk), dim3(kThreads), 0, st, mapping, nm,
-                     (const int64_t *)nullptr, (const int64_t *)nullptr, (int64_t)0, t, slot_of,
+  hipLaunchKernelGGL(k_scatter, dim3((unsigned)nblk), dim3(kThreads), 0, st, mapping, nmc,
+                     (const int64_t *)nullptr, (const int64_t *)nullptr, (int64_t)0, t, t.slot_of,
                      boff, nblk, unique, d_nunique);
   DGS_LAUNCH_CHECK();
   if (nr > 0) {
@@ -243,7 +198,7 @@ void relabel_generic(const int64_t *mapping, int64_t nm, const int64_t *req, int
     DGS_LAUNCH_CHECK();
   }
   if (nm > 0) {
-    hipLaunchKernelGGL(k_clear_slots, dim3((unsigned)nblk), dim3(kThreads), 0, st, t, slot_of,
+    hipLaunchKernelGGL(k_clear_slots, dim3((unsigned)nblk), dim3(kThreads), 0, st, t, t.slot_of,
                        nm);
     DGS_LAUNCH_CHECK();
   }

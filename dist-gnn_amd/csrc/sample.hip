@@ -19,21 +19,20 @@
 // Offsets come from a reduce-then-scan over 256-row tiles (no host sync inside the hop).
 #include "dgs_block.cuh"
 #include "dgs_ops.h"
+#include "dgs_table.cuh"
 
 namespace dgs {
 namespace {
 
 constexpr int kTileRows = 256;   // rows per prep / sample workgroup
 constexpr int kGroup = 16;       // lanes per row in the uniform kernel
+constexpr int kRowsPerBlock = kTileRows / kGroup;  // rows per uniform-sampling workgroup
 constexpr int kHubT = 1024;      // reservoir tail length above which a row is split
-constexpr int kHubBlocks = 512;  // workgroups of the hub kernel
+constexpr int kHubBlocks = 2048; // workgroups of the hub kernel (8 waves per SIMD)
 constexpr int kMaxPicksLds = 512;
 constexpr int kScanThreads = 1024;
 
-struct RowInfo {
-  int64_t off;
-  int64_t dl;  // degree | location << 56
-};
+using RowInfo = NodeEntry;  // {absolute neighbour-id pointer, degree | location << 56}
 
 __device__ __forceinline__ int64_t ri_deg(const RowInfo &r) { return r.dl & kOffMask; }
 __device__ __forceinline__ int ri_loc(const RowInfo &r) {
@@ -41,17 +40,27 @@ __device__ __forceinline__ int ri_loc(const RowInfo &r) {
 }
 
 __device__ __forceinline__ RowInfo lookup_row(const RowSrc &src, int64_t v) {
+  if (src.ntab) return src.ntab[v];
+  const int64_t b = src.indptr[v], e = src.indptr[v + 1];
   RowInfo ri;
-  if (src.ntab) {
-    const NodeEntry e = src.ntab[v];
-    ri.off = e.off;
-    ri.dl = e.dl;
-  } else {
-    const int64_t b = src.indptr[v], e = src.indptr[v + 1];
-    ri.off = b;
-    ri.dl = e - b;  // location 0
-  }
+  ri.ptr = src.indices + b;
+  ri.dl = e - b;  // location 0
   return ri;
+}
+
+// Probability array of a row: same offset as its neighbour ids inside the row's location.
+__device__ __forceinline__ const float *row_probs(const RowSrc &src, const RowInfo &ri) {
+  const int loc = ri_loc(ri);
+  const int64_t *ib = nullptr;
+  const float *pb = nullptr;
+#pragma unroll
+  for (int d = 0; d <= kMaxDevices; ++d) {
+    if (loc == d) {
+      ib = reinterpret_cast<const int64_t *>(src.indices_base.p[d]);
+      pb = reinterpret_cast<const float *>(src.probs.p[d]);
+    }
+  }
+  return pb + (ri.ptr - ib);
 }
 
 __device__ __forceinline__ int64_t row_count(int64_t deg, int64_t k, bool replace) {
@@ -75,19 +84,27 @@ struct HubView {
 };
 
 // ------------------------------------------------------------------------------------
-// Prep: per-row lookup (one 16-byte node-table load), counts, hub detection, tile sums.
+// Prep: per-row lookup (one 16-byte node-table load), per-row in-tile output prefix, tile
+// sums, hub detection (+ hub slot initialisation, slot s = s: rowwise_sampling.cu:80-82).
 __global__ __launch_bounds__(kTileRows) void k_prep(RowSrc src, const int64_t *__restrict__ seeds,
-                                                    int64_t S, int64_t k, int replace,
+                                                    Count Sc, int64_t k, int replace,
                                                     int use_hubs, int bias_replace,
                                                     RowInfo *__restrict__ rowinfo,
+                                                    int32_t *__restrict__ tpre,
+                                                    int32_t *__restrict__ tpre2,
                                                     int64_t *__restrict__ bsum,
-                                                    int64_t *__restrict__ tsum, HubView hub) {
+                                                    int64_t *__restrict__ tsum, HubView hub,
+                                                    int32_t *__restrict__ hubslot, Table table) {
   __shared__ int64_t lds[kTileRows / 64];
+  const int64_t S = Sc.get();
+  if ((int64_t)blockIdx.x * kTileRows >= S) return;  // whole workgroup past the live rows
   const int64_t i = (int64_t)blockIdx.x * kTileRows + threadIdx.x;
   int64_t cnt = 0, tdeg = 0;
   if (i < S) {
-    const RowInfo ri = lookup_row(src, seeds[i]);
+    const int64_t v = seeds[i];
+    const RowInfo ri = lookup_row(src, v);
     rowinfo[i] = ri;
+    table_record(table, v, i);
     const int64_t deg = ri_deg(ri);
     cnt = row_count(deg, k, replace);
     tdeg = deg;
@@ -97,38 +114,52 @@ __global__ __launch_bounds__(kTileRows) void k_prep(RowSrc src, const int64_t *_
         h = atomicAdd((unsigned long long *)hub.count, 1ull);
         hub.row[h] = i;
         hub.nch[h] = (deg - k + 511) / 512;
+        for (int64_t s2 = 0; s2 < k; ++s2) hubslot[h * k + s2] = (int32_t)s2;
       }
       hub.hubid[i] = h;
     }
   }
-  const int64_t s = block_sum<kTileRows>(cnt, lds);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = s;
+  int64_t tot;
+  const int64_t ex = block_exclusive_scan<kTileRows>(cnt, &tot, lds);
+  if (i < S) tpre[i] = (int32_t)ex;
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
   if (bias_replace) {
-    const int64_t t = block_sum<kTileRows>(tdeg, lds);
-    if (threadIdx.x == 0) tsum[blockIdx.x] = t;
+    const int64_t ex2 = block_exclusive_scan<kTileRows>(tdeg, &tot, lds);
+    if (i < S) tpre2[i] = (int32_t)ex2;
+    if (threadIdx.x == 0) tsum[blockIdx.x] = tot;
   }
 }
 
-// Single workgroup: exclusive scan of tile sums (-> boff[0..nb], boff[nb] = nnz), the hub
-// chunk prefix and hub slot initialisation (slot s = s, rowwise_sampling.cu:80-82).
-__global__ __launch_bounds__(kScanThreads) void k_scan_hop(const int64_t *bsum, int64_t nb,
-                                                          int64_t *boff, int use_hubs,
-                                                          HubView hub, int64_t k,
-                                                          int32_t *hubslot) {
+// Single workgroup: exclusive scan of tile sums (-> boff[0..nb], boff[nb] = nnz; the same for
+// the CDF sizes when biased-with-replacement) and the hub chunk prefix.
+__global__ __launch_bounds__(kScanThreads) void k_scan_hop(const int64_t *bsum,
+                                                          const int64_t *tsum, Count Sc,
+                                                          int64_t *boff, int64_t *tboff,
+                                                          int use_hubs, HubView hub,
+                                                          int64_t *d_nnz, int64_t *d_cdf_total) {
   __shared__ int64_t lds[kScanThreads / 64];
-  int64_t carry = 0;
-  for (int64_t base = 0; base < nb; base += kScanThreads) {
-    const int64_t i = base + threadIdx.x;
-    const int64_t v = i < nb ? bsum[i] : 0;
-    int64_t tot;
-    const int64_t ex = block_exclusive_scan<kScanThreads>(v, &tot, lds);
-    if (i < nb) boff[i] = carry + ex;
-    carry += tot;
+  const int64_t nb = (Sc.get() + kTileRows - 1) / kTileRows;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int64_t *in = pass ? tsum : bsum;
+    int64_t *out = pass ? tboff : boff;
+    if (!in) continue;
+    int64_t carry = 0;
+    for (int64_t base = 0; base < nb; base += kScanThreads) {
+      const int64_t i = base + threadIdx.x;
+      const int64_t v = i < nb ? in[i] : 0;
+      int64_t tot;
+      const int64_t ex = block_exclusive_scan<kScanThreads>(v, &tot, lds);
+      if (i < nb) out[i] = carry + ex;
+      carry += tot;
+    }
+    if (threadIdx.x == 0) {
+      out[nb] = carry;
+      *(pass ? d_cdf_total : d_nnz) = carry;
+    }
   }
-  if (threadIdx.x == 0) boff[nb] = carry;
   if (!use_hubs) return;
   const int64_t H = *hub.count;
-  carry = 0;
+  int64_t carry = 0;
   for (int64_t base = 0; base < H; base += kScanThreads) {
     const int64_t i = base + threadIdx.x;
     const int64_t v = i < H ? hub.nch[i] : 0;
@@ -138,7 +169,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_hop(const int64_t *bsum, 
     carry += tot;
   }
   if (threadIdx.x == 0) hub.cptr[H] = carry;
-  for (int64_t j = threadIdx.x; j < H * k; j += kScanThreads) hubslot[j] = (int32_t)(j % k);
 }
 
 // ------------------------------------------------------------------------------------
@@ -146,41 +176,54 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_hop(const int64_t *bsum, 
 // w < 4 <-> one Philox block per logical thread t) of any hub row and folds its picks into
 // the row's k slots with atomicMax (rowwise_sampling.cu:85-92).
 __global__ __launch_bounds__(256) void k_hub_reservoir(const RowInfo *__restrict__ rowinfo,
-                                                       int64_t S, int64_t k, uint64_t seed,
+                                                       Count Sc, int64_t k, uint64_t seed,
                                                        HubView hub, int32_t *hubslot) {
+  const int64_t S = Sc.get();
   const int64_t H = *hub.count;
   if (H == 0) return;
   const int64_t total = hub.cptr[H];
   const int lane = threadIdx.x & 63;
+  // Each wave owns one contiguous range of chunks: one binary search per wave, then the hub
+  // index only moves forward (a dependent search per chunk would dominate the Philox work).
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < total;
-       c += nwaves) {
-    int64_t lo = 0, hi = H;  // largest h with cptr[h] <= c
-    while (hi - lo > 1) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (hub.cptr[mid] <= c) lo = mid; else hi = mid;
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t c0 = total * gw / nwaves, c1 = total * (gw + 1) / nwaves;
+  if (c0 >= c1) return;
+  int64_t lo = 0, hi = H;  // largest h with cptr[h] <= c0
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (hub.cptr[mid] <= c0) lo = mid; else hi = mid;
+  }
+  int64_t h = lo;
+  int64_t hstart = hub.cptr[h], hnext = hub.cptr[h + 1];
+  int64_t r = hub.row[h];
+  int64_t deg = ri_deg(rowinfo[r]);
+  for (int64_t c = c0; c < c1; ++c) {
+    while (c >= hnext) {
+      ++h;
+      hstart = hnext;
+      hnext = hub.cptr[h + 1];
+      r = hub.row[h];
+      deg = ri_deg(rowinfo[r]);
     }
-    const int64_t h = lo;
-    const int64_t q = c - hub.cptr[h];
-    const int64_t r = hub.row[h];
-    const int64_t deg = ri_deg(rowinfo[r]);
-    const uint64_t key = seed * (uint64_t)S + (uint64_t)r;
+    const int64_t q = c - hstart;
+    const uint64_t key = wave_uniform(seed * (uint64_t)S + (uint64_t)r);
     const uint2 kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
     int32_t *sl = hubslot + h * k;
+    const uint4 o4a = philox4x32_10(
+        make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)lane, 0u), kk);
+    const uint4 o4b = philox4x32_10(
+        make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)(lane + 64), 0u), kk);
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
-      const int t = lane + 64 * tt;
-      const int64_t base = k + t + 512 * q;
-      if (base < deg) {
-        const uint4 o4 = philox4x32_10(make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32),
-                                                  (uint32_t)t, 0u), kk);
+      const uint4 o4 = tt ? o4b : o4a;
+      const int64_t base = k + lane + 64 * tt + 512 * q;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const int64_t idx = base + 128 * w;
-          if (idx < deg) {
-            const uint32_t num = u4_get(o4, w) % (uint32_t)(idx + 1);
-            if ((int64_t)num < k) atomicMax(sl + num, (int32_t)idx);
-          }
+      for (int w = 0; w < 4; ++w) {
+        const int64_t idx = base + 128 * w;
+        if (idx < deg) {
+          const uint32_t num = u4_get(o4, w) % (uint32_t)(idx + 1);
+          if ((int64_t)num < k) atomicMax(sl + num, (int32_t)idx);
         }
       }
     }
@@ -191,89 +234,83 @@ __global__ __launch_bounds__(256) void k_hub_reservoir(const RowInfo *__restrict
 // Uniform sampling of one 256-row tile.  16-lane groups own rows.
 template <bool kReplace>
 __global__ __launch_bounds__(kTileRows) void k_sample_uniform(
-    RowSrc src, int64_t S, int64_t k, uint64_t seed, const RowInfo *__restrict__ rowinfo,
-    const int64_t *__restrict__ boff, HubView hub, const int32_t *__restrict__ hubslot,
-    int use_hubs, int64_t *__restrict__ rowpos, int64_t *__restrict__ col) {
+    RowSrc src, Count Sc, int64_t k, uint64_t seed, const RowInfo *__restrict__ rowinfo,
+    const int32_t *__restrict__ tpre, const int64_t *__restrict__ boff, HubView hub,
+    const int32_t *__restrict__ hubslot, int use_hubs, int64_t *__restrict__ rowpos,
+    int64_t *__restrict__ col, Table table) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int64_t *s_off = reinterpret_cast<int64_t *>(smem);                       // [256]
-  int64_t *s_scan = s_off + kTileRows;                                       // [4]
-  int32_t *s_slot = reinterpret_cast<int32_t *>(s_scan + kTileRows / 64);   // [16][k]
-
-  const int64_t tile0 = (int64_t)blockIdx.x * kTileRows;
-  {
-    const int64_t i = tile0 + threadIdx.x;
-    const int64_t cnt = i < S ? row_count(ri_deg(rowinfo[i]), k, kReplace) : 0;
-    int64_t tot;
-    const int64_t ex = block_exclusive_scan<kTileRows>(cnt, &tot, s_scan);
-    s_off[threadIdx.x] = boff[blockIdx.x] + ex;
-  }
-  __syncthreads();
-
+  int32_t *s_slot = reinterpret_cast<int32_t *>(smem);  // [16 groups][k]
+  const int64_t S = Sc.get();
+  // the hub counter is consumed by now (k_hub_reservoir ran before this kernel): reset it for
+  // the next hop instead of a separate memset
+  if (use_hubs && blockIdx.x == 0 && threadIdx.x == 0) *hub.count = 0;
   const int g = threadIdx.x / kGroup, L = threadIdx.x % kGroup;
+  const int64_t r = (int64_t)blockIdx.x * kRowsPerBlock + g;
+  if (r >= S) return;
   int32_t *sl = s_slot + g * k;
-  for (int rr = g; rr < kTileRows; rr += kTileRows / kGroup) {
-    const int64_t r = tile0 + rr;
-    if (r >= S) break;
-    const RowInfo ri = rowinfo[r];
-    const int64_t deg = ri_deg(ri);
-    const int64_t begin = ri.off;
-    const int64_t *idx_base = reinterpret_cast<const int64_t *>(src.indices.p[ri_loc(ri)]);
-    const int64_t out = s_off[rr];
-    const uint64_t key = seed * (uint64_t)S + (uint64_t)r;
-    const uint2 kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
-    if (kReplace) {
-      if (deg > 0) {
-        for (int64_t p = L; p < k; p += kGroup) {
-          const int64_t t = p & 127, j = p >> 7;
-          const uint4 o4 = philox4x32_10(
-              make_uint4((uint32_t)(j >> 2), 0u, (uint32_t)t, 0u), kk);
-          const uint32_t x = u4_get(o4, (int)(j & 3));
-          const int64_t e = (int64_t)x % deg;
-          rowpos[out + p] = r;
-          col[out + p] = idx_base[begin + e];
-        }
-      }
-    } else if (deg <= k) {
-      for (int64_t p = L; p < deg; p += kGroup) {
+  const RowInfo ri = rowinfo[r];
+  const int64_t deg = ri_deg(ri);
+  const int64_t *nb = ri.ptr;
+  const int64_t out = boff[r / kTileRows] + tpre[r];
+  const uint64_t key = seed * (uint64_t)S + (uint64_t)r;
+  const uint2 kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
+  if (kReplace) {
+    if (deg > 0) {
+      for (int64_t p = L; p < k; p += kGroup) {
+        const int64_t t = p & 127, j = p >> 7;
+        const uint4 o4 = philox4x32_10(make_uint4((uint32_t)(j >> 2), 0u, (uint32_t)t, 0u), kk);
+        const uint32_t x = u4_get(o4, (int)(j & 3));
+        const int64_t e = (int64_t)x % deg;
+        const int64_t v = nb[e];
         rowpos[out + p] = r;
-        col[out + p] = idx_base[begin + p];
+        col[out + p] = v;
+        table_record(table, v, S + out + p);
       }
-    } else {
-      const int64_t h = use_hubs ? hub.hubid[r] : -1;
-      const int32_t *slots = sl;
-      if (h >= 0) {
-        slots = hubslot + h * k;
-      } else {
-        for (int64_t s = L; s < k; s += kGroup) sl[s] = (int32_t)s;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        for (int64_t q = 0; k + 512 * q < deg; ++q) {
-          for (int tt = 0; tt < 128 / kGroup; ++tt) {
-            const int t = L + kGroup * tt;
-            const int64_t base = k + t + 512 * q;
-            if (base >= deg) break;
-            const uint4 o4 = philox4x32_10(
-                make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)t, 0u), kk);
+    }
+    return;
+  }
+  if (deg <= k) {
+    for (int64_t p = L; p < deg; p += kGroup) {
+      const int64_t v = nb[p];
+      rowpos[out + p] = r;
+      col[out + p] = v;
+      table_record(table, v, S + out + p);
+    }
+    return;
+  }
+  const int64_t h = use_hubs ? hub.hubid[r] : -1;
+  const int32_t *slots = sl;
+  if (h >= 0) {
+    slots = hubslot + h * k;
+  } else {
+    for (int64_t s2 = L; s2 < k; s2 += kGroup) sl[s2] = (int32_t)s2;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int64_t q = 0; k + 512 * q < deg; ++q) {
+      for (int tt = 0; tt < 128 / kGroup; ++tt) {
+        const int t = L + kGroup * tt;
+        const int64_t base = k + t + 512 * q;
+        if (base >= deg) break;
+        const uint4 o4 = philox4x32_10(
+            make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)t, 0u), kk);
 #pragma unroll
-            for (int w = 0; w < 4; ++w) {
-              const int64_t idx = base + 128 * w;
-              if (idx < deg) {
-                const uint32_t num = u4_get(o4, w) % (uint32_t)(idx + 1);
-                if ((int64_t)num < k) atomicMax(sl + num, (int32_t)idx);
-              }
-            }
+        for (int w = 0; w < 4; ++w) {
+          const int64_t idx = base + 128 * w;
+          if (idx < deg) {
+            const uint32_t num = u4_get(o4, w) % (uint32_t)(idx + 1);
+            if ((int64_t)num < k) atomicMax(sl + num, (int32_t)idx);
           }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
       }
-      for (int64_t s = L; s < k; s += kGroup) {
-        rowpos[out + s] = r;
-        col[out + s] = idx_base[begin + slots[s]];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  for (int64_t s2 = L; s2 < k; s2 += kGroup) {
+    const int64_t v = nb[slots[s2]];
+    rowpos[out + s2] = r;
+    col[out + s2] = v;
+    table_record(table, v, S + out + s2);
   }
 }
 
@@ -325,40 +362,25 @@ __device__ __forceinline__ T float_max(T a, T b) {
   return fmaxf(a, b);
 }
 
+constexpr int kBiasRowsPerBlock = kTileRows / 32;  // one 32-lane half-wave per row
+
 template <bool kReplace>
 __global__ __launch_bounds__(kTileRows) void k_sample_bias(
-    RowSrc src, int64_t S, int64_t k, uint64_t seed, const RowInfo *__restrict__ rowinfo,
-    const int64_t *__restrict__ boff, const int64_t *__restrict__ tboff, float *cdf,
-    int64_t *__restrict__ rowpos, int64_t *__restrict__ col) {
-  __shared__ int64_t s_off[kTileRows];
-  __shared__ int64_t s_toff[kTileRows];
-  __shared__ int64_t s_scan[kTileRows / 64];
-  const int64_t tile0 = (int64_t)blockIdx.x * kTileRows;
-  {
-    const int64_t i = tile0 + threadIdx.x;
-    const int64_t deg = i < S ? ri_deg(rowinfo[i]) : 0;
-    int64_t tot;
-    const int64_t ex = block_exclusive_scan<kTileRows>(row_count(deg, k, kReplace), &tot, s_scan);
-    s_off[threadIdx.x] = boff[blockIdx.x] + ex;
-    if (kReplace) {
-      const int64_t ex2 = block_exclusive_scan<kTileRows>(deg, &tot, s_scan);
-      s_toff[threadIdx.x] = tboff[blockIdx.x] + ex2;
-    }
-  }
-  __syncthreads();
-
+    RowSrc src, Count Sc, int64_t k, uint64_t seed, const RowInfo *__restrict__ rowinfo,
+    const int32_t *__restrict__ tpre, const int64_t *__restrict__ boff,
+    const int32_t *__restrict__ tpre2, const int64_t *__restrict__ tboff, float *cdf,
+    int64_t *__restrict__ rowpos, int64_t *__restrict__ col, Table table) {
+  const int64_t S = Sc.get();
   const int64_t G = (S + 15) / 16;  // reference grid: ceil(S / TILE_SIZE=16)
   const int hw = threadIdx.x >> 5, l = threadIdx.x & 31;
-  for (int rr = hw; rr < kTileRows; rr += kTileRows / 32) {
-    const int64_t r = tile0 + rr;
-    if (r >= S) break;
+  {
+    const int64_t r = (int64_t)blockIdx.x * kBiasRowsPerBlock + hw;
+    if (r >= S) return;
     const RowInfo ri = rowinfo[r];
     const int64_t deg = ri_deg(ri);
-    const int64_t begin = ri.off;
-    const int loc = ri_loc(ri);
-    const int64_t *idx_base = reinterpret_cast<const int64_t *>(src.indices.p[loc]);
-    const float *p_base = reinterpret_cast<const float *>(src.probs.p[loc]);
-    const int64_t out = s_off[rr];
+    const int64_t *nb = ri.ptr;
+    const float *pr = row_probs(src, ri);
+    const int64_t out = boff[r / kTileRows] + tpre[r];
     // reference coordinates: block b = r / 16, warp w = (r % 16) % 4, chain position m
     const int64_t b = r / 16;
     const int w = (int)((r % 16) & 3), m = (int)((r % 16) >> 2);
@@ -378,10 +400,12 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
     if (!kReplace) {
       if (deg <= k) {
         for (int64_t p = l; p < deg; p += 32) {
+          const int64_t v = nb[p];
           rowpos[out + p] = r;
-          col[out + p] = idx_base[begin + p];
+          col[out + p] = v;
+          table_record(table, v, S + out + p);
         }
-        continue;
+        return;
       }
       // half-wave top-k: lane q holds the q-th best (key, idx) so far
       float bk = -__builtin_inff();
@@ -402,7 +426,7 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
             cached_q = q;
           }
           const float u = curand_uniform_from(u4_get(o4, (int)(j & 3)));
-          key_i = ares_key(u, p_base[begin + i]);
+          key_i = ares_key(u, pr[i]);
           ++j;
         }
         bool cand = i < deg && (cnt < k || ares_better(key_i, i, thr_k, thr_i));
@@ -433,18 +457,20 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
         }
       }
       if (l < k) {
+        const int64_t v = nb[bi];
         rowpos[out + l] = r;
-        col[out + l] = idx_base[begin + bi];
+        col[out + l] = v;
+        table_record(table, v, S + out + l);
       }
     } else {
-      if (deg == 0) continue;
+      if (deg == 0) return;
       // CDF, 32 edges at a time: lane 0 adds the running aggregate, clamp at 0, then a
       // Kogge-Stone inclusive scan (cub::WarpScan::InclusiveSum), :185-202.
-      float *crow = cdf + s_toff[rr];
+      float *crow = cdf + tboff[r / kTileRows] + tpre2[r];
       float agg = 0.0f, sum = 0.0f;
       for (int64_t base = 0; base < deg; base += 32) {
         const int64_t i = base + l;
-        float v = i < deg ? p_base[begin + i] : 0.0f;
+        float v = i < deg ? pr[i] : 0.0f;
         if (l == 0) v = __fadd_rn(v, agg);
         v = float_max(v, 0.0f);
 #pragma unroll
@@ -480,8 +506,10 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
           }
         }
         const int64_t item = ret < deg - 1 ? ret : deg - 1;
+        const int64_t v = nb[item];
         rowpos[out + p] = r;
-        col[out + p] = idx_base[begin + item];
+        col[out + p] = v;
+        table_record(table, v, S + out + p);
       }
     }
   }
@@ -490,10 +518,11 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
 }  // namespace
 
 // ------------------------------------------------------------------------------------
-void sample_hop(const RowSrc &src, const int64_t *seeds, int64_t S, int64_t k, bool replace,
+void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bool replace,
                 bool bias, uint64_t launch_seed, int64_t *rowpos, int64_t *col, int64_t *d_nnz,
-                HopScratch &ws, hipStream_t st) {
+                const Table &table, HopScratch &ws, hipStream_t st) {
   DGS_CHECK(k >= 0, "num_picks must be non-negative");
+  const int64_t S = Sc.v;  // exact when Sc.p == nullptr, else an upper bound
   DGS_CHECK(S < (int64_t(1) << 31), "too many seeds in one hop");
   const int64_t nb = ceil_div(S > 0 ? S : 1, kTileRows);
   ws.rowinfo.ensure(sizeof(RowInfo) * (size_t)(S > 0 ? S : 1));
@@ -504,61 +533,71 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, int64_t S, int64_t k, b
   int64_t *boff = ws.boff.as<int64_t>();
   int64_t *tboff = boff + nb + 1;
   RowInfo *rowinfo = ws.rowinfo.as<RowInfo>();
-  if (S == 0 || k == 0) {
+  if (S == 0) {
     DGS_HIP(hipMemsetAsync(d_nnz, 0, sizeof(int64_t), st));
     return;
   }
-  const bool use_hubs = !bias && !replace;
+  const bool use_hubs = !bias && !replace && k > 0;
+  // the hub counter lives in its own buffer: zeroed at allocation, then reset on the device by
+  // every hop that used it
+  if (ws.hubcount.ensure(64)) DGS_HIP(hipMemsetAsync(ws.hubcount.p, 0, 64, st));
   ws.hub.ensure(HubView::bytes(S));
   HubView hub = HubView::make(ws.hub.as<int64_t>(), S);
-  if (use_hubs) {
-    DGS_HIP(hipMemsetAsync(hub.count, 0, sizeof(int64_t), st));
-    ws.hubslot.ensure(sizeof(int32_t) * (size_t)(S * k));
-  }
+  hub.count = ws.hubcount.as<int64_t>();
   const bool bias_replace = bias && replace;
+  ws.tpre.ensure(sizeof(int32_t) * (size_t)(2 * S));
+  int32_t *tpre = ws.tpre.as<int32_t>();
+  int32_t *tpre2 = tpre + S;
+  if (use_hubs) ws.hubslot.ensure(sizeof(int32_t) * (size_t)(S * k));
   profile_begin(st, 1);
-  hipLaunchKernelGGL(k_prep, dim3((unsigned)nb), dim3(kTileRows), 0, st, src, seeds, S, k,
-                     (int)replace, (int)use_hubs, (int)bias_replace, rowinfo, bsum, tsum, hub);
+  hipLaunchKernelGGL(k_prep, dim3((unsigned)nb), dim3(kTileRows), 0, st, src, seeds, Sc, k,
+                     (int)replace, (int)use_hubs, (int)bias_replace, rowinfo, tpre, tpre2, bsum,
+                     tsum, hub, ws.hubslot.as<int32_t>(), table);
   DGS_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_scan_hop, dim3(1), dim3(kScanThreads), 0, st, bsum, nb, boff,
-                     (int)use_hubs, hub, k, ws.hubslot.as<int32_t>());
+  if (k == 0) {  // seeds still enter the relabel table (frontier = unique(seeds))
+    DGS_HIP(hipMemsetAsync(d_nnz, 0, sizeof(int64_t), st));
+    profile_end(st, 1);
+    return;
+  }
+  hipLaunchKernelGGL(k_scan_hop, dim3(1), dim3(kScanThreads), 0, st, bsum,
+                     bias_replace ? (const int64_t *)tsum : nullptr, Sc, boff, tboff,
+                     (int)use_hubs, hub, d_nnz, bsum + 2 * nb + 1);
   DGS_LAUNCH_CHECK();
-  DGS_HIP(hipMemcpyAsync(d_nnz, boff + nb, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
 
   if (!bias) {
     if (use_hubs) {
-      hipLaunchKernelGGL(k_hub_reservoir, dim3(kHubBlocks), dim3(256), 0, st, rowinfo, S, k,
+      hipLaunchKernelGGL(k_hub_reservoir, dim3(kHubBlocks), dim3(256), 0, st, rowinfo, Sc, k,
                          launch_seed, hub, ws.hubslot.as<int32_t>());
       DGS_LAUNCH_CHECK();
     }
     DGS_CHECK(replace || k <= kMaxPicksLds, "num_picks > 512 is not supported without replacement");
-    const size_t lds = sizeof(int64_t) * (kTileRows + kTileRows / 64) +
-                       (replace ? 0 : sizeof(int32_t) * (size_t)(kTileRows / kGroup) * k);
+    const size_t lds = replace ? 16 : sizeof(int32_t) * (size_t)kRowsPerBlock * k;
+    const dim3 grid((unsigned)ceil_div(S, kRowsPerBlock));
     if (replace)
-      hipLaunchKernelGGL(k_sample_uniform<true>, dim3((unsigned)nb), dim3(kTileRows), lds, st,
-                         src, S, k, launch_seed, rowinfo, boff, hub, ws.hubslot.as<int32_t>(),
-                         0, rowpos, col);
+      hipLaunchKernelGGL(k_sample_uniform<true>, grid, dim3(kTileRows), lds, st, src, Sc, k,
+                         launch_seed, rowinfo, tpre, boff, hub, ws.hubslot.as<int32_t>(), 0,
+                         rowpos, col, table);
     else
-      hipLaunchKernelGGL(k_sample_uniform<false>, dim3((unsigned)nb), dim3(kTileRows), lds, st,
-                         src, S, k, launch_seed, rowinfo, boff, hub, ws.hubslot.as<int32_t>(),
-                         1, rowpos, col);
+      hipLaunchKernelGGL(k_sample_uniform<false>, grid, dim3(kTileRows), lds, st, src, Sc, k,
+                         launch_seed, rowinfo, tpre, boff, hub, ws.hubslot.as<int32_t>(), 1,
+                         rowpos, col, table);
     DGS_LAUNCH_CHECK();
   } else {
     DGS_CHECK(k <= 32, "biased sampling supports num_picks <= 32 (rowwise_sampling_bias.cu:73)");
     float *cdf = nullptr;
+    const dim3 grid((unsigned)ceil_div(S, kBiasRowsPerBlock));
     if (replace) {
       // CDF scratch = sum of degrees (the reference's temp tensor, :257-259): one D2H.
-      scan_small(tsum, nb, tboff, st);
-      int64_t *h = (ws.host.ensure(16), ws.host.as<int64_t>());
-      DGS_HIP(hipMemcpyAsync(h, tboff + nb, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      int64_t *h = (ws.host.ensure(64), ws.host.as<int64_t>() + 4);
+      DGS_HIP(hipMemcpyAsync(h, bsum + 2 * nb + 1, sizeof(int64_t), hipMemcpyDeviceToHost, st));
       DGS_HIP(hipStreamSynchronize(st));
       ws.cdf.ensure(sizeof(float) * (size_t)(h[0] > 0 ? h[0] : 1));
       cdf = ws.cdf.as<float>();
-      hipLaunchKernelGGL(k_sample_bias<true>, dim3((unsigned)nb), dim3(kTileRows), 0, st, src, S,
-                         k, launch_seed, rowinfo, boff, tboff, cdf, rowpos, col);
+      hipLaunchKernelGGL(k_sample_bias<true>, grid, dim3(kTileRows), 0, st, src, Sc, k,
+                         launch_seed, rowinfo, tpre, boff, tpre2, tboff, cdf, rowpos, col, table);
     } else {
-      hipLaunchKernelGGL(k_sample_bias<false>, dim3((unsigned)nb), dim3(kTileRows), 0, st, src,
-                         S, k, launch_seed, rowinfo, boff, tboff, cdf, rowpos, col);
+      hipLaunchKernelGGL(k_sample_bias<false>, grid, dim3(kTileRows), 0, st, src, Sc, k,
+                         launch_seed, rowinfo, tpre, boff, tpre2, tboff, cdf, rowpos, col, table);
     }
     DGS_LAUNCH_CHECK();
   }

@@ -131,23 +131,24 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
   // graph shard context: node table (replaces CreateNidsP2PCacheHashMapCUDA, hashmap.cu)
   ntab_.ensure(sizeof(NodeEntry) * (size_t)(num_nodes > 0 ? num_nodes : 1));
   NodeEntry *ntab = ntab_.as<NodeEntry>();
-  ntab_init_host(ntab, d_indptr, num_nodes, st);
+  ntab_init_host(ntab, d_indptr, num_nodes, (const int64_t *)h_indices_.dev, st);
   for (int d : rotation(rank_, world_))
     ntab_assign(ntab, (const int64_t *)nids_srv_->ptr(d), (const int64_t *)indptr_srv_->ptr(d),
-                nids_srv_->items(d), d, st);
+                nids_srv_->items(d), d, (const int64_t *)indices_srv_->ptr(d), st);
   DGS_HIP(hipStreamSynchronize(st));
 
   src_.ntab = ntab;
   src_.indptr = nullptr;
+  src_.indices = nullptr;
   for (int d = 0; d <= kMaxDevices; ++d) {
-    src_.indices.p[d] = nullptr;
+    src_.indices_base.p[d] = nullptr;
     src_.probs.p[d] = nullptr;
   }
   for (int d = 0; d < world_; ++d) {
-    src_.indices.p[d] = indices_srv_->ptr(d);
+    src_.indices_base.p[d] = indices_srv_->ptr(d);
     src_.probs.p[d] = bias_ ? probs_srv_->ptr(d) : nullptr;
   }
-  src_.indices.p[kLocHost] = h_indices_.dev;
+  src_.indices_base.p[kLocHost] = h_indices_.dev;
   src_.probs.p[kLocHost] = bias_ ? h_probs_.dev : nullptr;
 }
 
@@ -160,50 +161,69 @@ Sampler::~Sampler() {
 
 void Sampler::bounds(int64_t n_seeds, const int64_t *fan_out, int L, int64_t *fcap,
                      int64_t *ecap) const {
+  // frontier_h <= S_h * (1 + k) and, being unique node ids, <= N (the first hop's seeds may
+  // repeat, so its bound keeps S_0 in).
   int64_t s = n_seeds;
   for (int h = 0; h < L; ++h) {
     const int64_t k = fan_out[L - 1 - h];
     const int64_t e = s * k;
     ecap[h] = e;
     s = s + e;
+    if (s > num_nodes_ && num_nodes_ > 0) s = std::max<int64_t>(num_nodes_, 1);
     fcap[h] = s;
   }
 }
 
 // sampler.cc:14-62, 146-166: hops run fan_out[L-1] .. fan_out[0]; seeds <- frontier.
+// All hops are enqueued without host synchronisation: hop h+1 reads its seed count from the
+// device word the relabel of hop h wrote, grids are sized by the host-side upper bounds, and
+// the per-hop sizes come back in one D2H copy at the end.
 void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_out, int L,
                      bool replace, int64_t *const *frontiers, int64_t *const *rows,
                      int64_t *const *cols, int64_t *sizes, hipStream_t st) {
-  sizes_.ensure(4 * sizeof(int64_t));
-  ws_.host.ensure(4 * sizeof(int64_t));
+  if (L <= 0) return;
+  sizes_.ensure(sizeof(int64_t) * (size_t)(3 * L + 1));
+  sizes_host_.ensure(sizeof(int64_t) * (size_t)(3 * L + 1));
   int64_t *dsz = sizes_.as<int64_t>();
-  int64_t *hsz = ws_.host.as<int64_t>();
+  int64_t *hsz = sizes_host_.as<int64_t>();
+  std::vector<int64_t> fcap(L), ecap(L);
+  bounds(n_seeds, fan_out, L, fcap.data(), ecap.data());
+  int64_t max_e = 1;
+  for (int h = 0; h < L; ++h) max_e = std::max(max_e, ecap[h]);
+  rowpos_.ensure(sizeof(int64_t) * (size_t)max_e);
   const int64_t *cur = seeds;
-  int64_t S = n_seeds;
+  Count S{n_seeds, nullptr};
   for (int h = 0; h < L; ++h) {
     const int64_t k = fan_out[L - 1 - h];
     DGS_CHECK(k >= 0, "fan_out entries must be non-negative");
     const uint64_t seed = rng().next();
-    const int64_t nnz_cap = S * k;
-    rowpos_.ensure(sizeof(int64_t) * (size_t)(nnz_cap > 0 ? nnz_cap : 1));
-    sample_hop(src_, cur, S, k, replace, bias_, seed, rowpos_.as<int64_t>(), cols[h], dsz, ws_,
-               st);
-    relabel_hop(cur, S, cols[h], dsz, nnz_cap, rowpos_.as<int64_t>(), frontiers[h], rows[h],
-                cols[h], dsz + 1, ws_, st);
-    DGS_HIP(hipMemcpyAsync(hsz, dsz, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    DGS_HIP(hipStreamSynchronize(st));
-    sizes[3 * h + 0] = S;
-    sizes[3 * h + 1] = hsz[1];
-    sizes[3 * h + 2] = hsz[0];
+    const int64_t nnz_cap = ecap[h];
+    int64_t *d_nnz = dsz + 3 * h + 2;
+    int64_t *d_uniq = dsz + 3 * h + 1;
+    const Table t = relabel_table(ws_, S.v + nnz_cap, st);
+    ws_.table_dirty = true;
+    sample_hop(src_, cur, S, k, replace, bias_, seed, rowpos_.as<int64_t>(), cols[h], d_nnz, t,
+               ws_, st);
+    relabel_hop(cur, S, cols[h], d_nnz, nnz_cap, rowpos_.as<int64_t>(), t, frontiers[h], rows[h],
+                cols[h], d_uniq, ws_, st);
     cur = frontiers[h];
-    S = hsz[1];
+    S = Count{fcap[h], d_uniq};
+  }
+  DGS_HIP(hipMemcpyAsync(hsz, dsz, sizeof(int64_t) * (size_t)(3 * L), hipMemcpyDeviceToHost, st));
+  DGS_HIP(hipStreamSynchronize(st));
+  int64_t s = n_seeds;
+  for (int h = 0; h < L; ++h) {
+    sizes[3 * h + 0] = s;
+    sizes[3 * h + 1] = hsz[3 * h + 1];
+    sizes[3 * h + 2] = hsz[3 * h + 2];
+    s = hsz[3 * h + 1];
   }
 }
 
 void Sampler::build_cache_rowtab(int64_t *tab, hipStream_t st) const {
-  ftab_init_host(tab, num_nodes_, st);
+  loctab_init_host(tab, num_nodes_, st);
   for (int d : rotation(rank_, world_))
-    ftab_assign(tab, (const int64_t *)nids_srv_->ptr(d), nids_srv_->items(d), d, st);
+    loctab_assign(tab, (const int64_t *)nids_srv_->ptr(d), nids_srv_->items(d), d, st);
 }
 
 int64_t Sampler::cache_map_size() const {
@@ -256,6 +276,7 @@ FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_byt
   feat_srv_ = P2PServer::adopt(block, n_cache, row_bytes);
 
   std::vector<int64_t> nbytes(world_, n_cache * 8);
+  DGS_CHECK(world_ <= kMaxDevices, "at most 8 GPUs");
   std::vector<void *> lists(world_, nullptr);
   if (world_ > 1) {
     lists = c.allgather_device(nids, n_cache * 8, &nbytes);
@@ -264,22 +285,23 @@ FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_byt
   }
   ftab_.ensure(sizeof(int64_t) * (size_t)(num_rows > 0 ? num_rows : 1));
   int64_t *ftab = ftab_.as<int64_t>();
-  ftab_init_host(ftab, num_rows, st);
-  for (int d : rotation(rank_, world_))
-    ftab_assign(ftab, (const int64_t *)lists[d], nbytes[d] / 8, d, st);
+  // absolute row addresses: host rows first, then every GPU's cache (local last = priority)
+  ftab_init(ftab, num_rows, h_data_.dev, row_bytes, st);
+  align_or_ = (uintptr_t)h_data_.dev;
+  for (int d : rotation(rank_, world_)) {
+    ftab_assign(ftab, (const int64_t *)lists[d], nbytes[d] / 8, feat_srv_->ptr(d), row_bytes, st);
+    align_or_ |= (uintptr_t)feat_srv_->ptr(d);
+  }
   DGS_HIP(hipStreamSynchronize(st));
   if (world_ > 1)
     for (void *p : lists) DGS_HIP(hipFree(p));
   DGS_HIP(hipFree(nids));
-  for (int d = 0; d <= kMaxDevices; ++d) bases_.p[d] = nullptr;
-  for (int d = 0; d < world_; ++d) bases_.p[d] = feat_srv_->ptr(d);
-  bases_.p[kLocHost] = h_data_.dev;
 }
 
 FeatureServer::~FeatureServer() { delete feat_srv_; }
 
 void FeatureServer::gather(const int64_t *nids, int64_t n, void *out, hipStream_t st) const {
-  gather_table(ftab_.as<int64_t>(), bases_, row_bytes_, nids, n, out, st);
+  gather_table(ftab_.as<int64_t>(), align_or_, row_bytes_, nids, n, out, st);
 }
 
 }  // namespace dgs

@@ -3,6 +3,7 @@
 // src/feature/feature_server.cc).
 #pragma once
 
+#include <algorithm>
 #include <vector>
 
 #include "context.h"
@@ -82,6 +83,7 @@ class Sampler {
   RowSrc src_{};
   HopScratch ws_;
   DevBuf rowpos_, sizes_;
+  HostPinned sizes_host_;
 };
 
 class FeatureServer {
@@ -99,7 +101,7 @@ class FeatureServer {
   HostView h_data_;
   P2PServer *feat_srv_ = nullptr;
   DevBuf ftab_;
-  PtrTable bases_{};
+  uintptr_t align_or_ = 0;
 };
 
 }  // namespace dgs

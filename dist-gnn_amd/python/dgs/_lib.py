@@ -67,7 +67,8 @@ _SIGS = {
     "dgs_feature_server_local_cache": (c_int, [c_vp, p_vp, p_i64]),
     "dgs_feature_server_destroy": (c_int, [c_vp]),
     "dgs_profile_enable": (c_int, [c_int]),
-    "dgs_profile_read": (c_int, [ctypes.POINTER(c_dbl), p_i64, ctypes.POINTER(c_dbl), p_i64]),
+    "dgs_profile_read": (c_int, [ctypes.POINTER(c_dbl), p_i64, ctypes.POINTER(c_dbl), p_i64,
+                                 ctypes.POINTER(c_dbl), p_i64]),
 }
 
 for _name, (_res, _args) in _SIGS.items():

@@ -79,35 +79,50 @@ class P2PCacheSampler:
         check(lib.dgs_sampler_create(ptr(ip), ptr(ix), ptr(pr), self.num_nodes, ix.numel(),
                                      ptr(cn), cn.numel(), int(device_id), ctypes.byref(h)))
         self._h = h
+        self._plans = {}
         self.device = torch.device("cuda", torch.cuda.current_device())
 
     def _CAPI_sample_node_classifiction(self, seeds, fan_out, replace=False):
         """sampler.cc:146-166 -> [(seeds, frontier, coo_row, coo_col)] per hop
         (hop h samples fan_out[L-1-h]); coo ids are local to (frontier, seeds)."""
         check_cuda(seeds, "seeds")
-        s = as_i64(seeds, "seeds")
+        s = seeds if seeds.dtype == torch.int64 and seeds.is_contiguous() else \
+            as_i64(seeds, "seeds")
         L = len(fan_out)
         if L == 0:
             return []
-        fo = i64_array(fan_out)
-        fcap, ecap = (c_i64 * L)(), (c_i64 * L)()
-        check(lib.dgs_sampler_bounds(self._h, s.numel(), fo, L, fcap, ecap))
-        dev = s.device
-        fronts = [torch.empty(int(fcap[h]), dtype=torch.int64, device=dev) for h in range(L)]
-        rows = [torch.empty(int(ecap[h]), dtype=torch.int64, device=dev) for h in range(L)]
-        cols = [torch.empty(int(ecap[h]), dtype=torch.int64, device=dev) for h in range(L)]
+        key = (tuple(fan_out), s.numel())
+        plan = self._plans.get(key)
+        if plan is None:
+            fo = i64_array(fan_out)
+            fcap, ecap = (c_i64 * L)(), (c_i64 * L)()
+            check(lib.dgs_sampler_bounds(self._h, s.numel(), fo, L, fcap, ecap))
+            caps = [(int(fcap[h]), int(ecap[h])) for h in range(L)]
+            plan = (fo, caps, sum(f + 2 * e for f, e in caps))
+            self._plans[key] = plan
+        fo, caps, total = plan
+        # one allocation for every hop's (frontier, row, col) buffers
+        buf = torch.empty(max(total, 1), dtype=torch.int64, device=s.device)
+        base, off = buf.data_ptr(), 0
+        fr_p, row_p, col_p, views = [], [], [], []
+        for f, e in caps:
+            views.append((off, f, off + f, e, off + f + e))
+            fr_p.append(base + 8 * off)
+            row_p.append(base + 8 * (off + f))
+            col_p.append(base + 8 * (off + f + e))
+            off += f + 2 * e
         sizes = (c_i64 * (3 * L))()
-        check(lib.dgs_sampler_sample(self._h, ptr(s), s.numel(), fo, L, int(bool(replace)),
-                                     vp_array([t.data_ptr() for t in fronts]),
-                                     vp_array([t.data_ptr() for t in rows]),
-                                     vp_array([t.data_ptr() for t in cols]), sizes,
-                                     stream_ptr(dev)))
+        check(lib.dgs_sampler_sample(self._h, c_vp(s.data_ptr()), s.numel(), fo, L,
+                                     int(bool(replace)), vp_array(fr_p), vp_array(row_p),
+                                     vp_array(col_p), sizes, stream_ptr(s.device)))
         out = []
         cur = seeds
         cast = self._id_dtype != torch.int64
-        for h in range(L):
-            U, nnz = int(sizes[3 * h + 1]), int(sizes[3 * h + 2])
-            fr, r, c = fronts[h][:U], rows[h][:nnz], cols[h][:nnz]
+        for h, (fo_off, _, ro_off, e, co_off) in enumerate(views):
+            U, nnz = sizes[3 * h + 1], sizes[3 * h + 2]
+            fr = buf[fo_off:fo_off + U]
+            r = buf[ro_off:ro_off + nnz]
+            c = buf[co_off:co_off + nnz]
             if cast:
                 fr, r, c = fr.to(self._id_dtype), r.to(self._id_dtype), c.to(self._id_dtype)
             out.append((cur, fr, r, c))
@@ -184,10 +199,10 @@ class P2PCacheFeatureServer:
     def _CAPI_get_feature(self, nids):
         """feature_server.cc:69-74 -> [n, stride] (2-D, feature_ops.cu:110-112)."""
         check_cuda(nids, "nids")
-        n = as_i64(nids, "nids")
+        n = nids if nids.dtype == torch.int64 and nids.is_contiguous() else as_i64(nids, "nids")
         out = torch.empty((n.numel(), self._stride), dtype=self._dtype, device=n.device)
-        check(lib.dgs_feature_server_gather(self._h, ptr(n), n.numel(), ptr(out),
-                                            stream_ptr(n.device)))
+        check(lib.dgs_feature_server_gather(self._h, c_vp(n.data_ptr()), n.numel(),
+                                            c_vp(out.data_ptr()), stream_ptr(n.device)))
         return out
 
     def __del__(self):

@@ -230,10 +230,11 @@ def profile_enable(on=True):
 
 def profile_read():
     gm, gn, sm, sn = ctypes.c_double(), c_i64(), ctypes.c_double(), c_i64()
+    xm, xn = ctypes.c_double(), c_i64()
     check(lib.dgs_profile_read(ctypes.byref(gm), ctypes.byref(gn), ctypes.byref(sm),
-                               ctypes.byref(sn)))
+                               ctypes.byref(sn), ctypes.byref(xm), ctypes.byref(xn)))
     return {"gather_ms": gm.value, "gather_launches": gn.value, "sample_ms": sm.value,
-            "sample_calls": sn.value}
+            "sample_calls": sn.value, "select_ms": xm.value, "select_launches": xn.value}
 
 
 _lib  # noqa: B018  (keep module import for side effects)

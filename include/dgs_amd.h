@@ -166,13 +166,14 @@ int dgs_feature_server_local_cache(const dgs_feature_server *s, const void **ptr
 int dgs_feature_server_destroy(dgs_feature_server *s);
 
 /* ------------------------------------------------------------------------------------
- * Instrumentation (bench.py): time the hot kernels with HIP events on the stream they run
- * on.  When enabled, the library records events around its gather kernel and sums their
- * durations; dgs_profile_read() returns (total_ms, launches) and resets.
+ * Instrumentation (bench.py).  When enabled, gather kernels are launched with
+ * hipExtLaunchKernelGGL start/stop events (recorded by the GPU at the kernel's own start and
+ * end, on the stream it runs on) and every sampling hop is bracketed by stream events.
+ * dgs_profile_read() returns the summed milliseconds and counts, then resets them.
  * ---------------------------------------------------------------------------------- */
 int dgs_profile_enable(int on);
 int dgs_profile_read(double *gather_ms, int64_t *gather_launches, double *sample_ms,
-                     int64_t *sample_calls);
+                     int64_t *sample_calls, double *select_ms, int64_t *select_launches);
 
 #ifdef __cplusplus
 }
