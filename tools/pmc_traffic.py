@@ -1,0 +1,66 @@
+"""Derives per-launch HBM traffic of the feature-gather kernel from rocprofv3 PMC CSVs.
+
+Inputs: counter_collection CSVs of four runs -- {bench, calibration} x {FETCH_SIZE,
+WRITE_SIZE} (separate passes: FETCH_SIZE uses 3 TCC slots, WRITE_SIZE 2).  FETCH_SIZE /
+WRITE_SIZE are in KiB.  The read-side factor comes from the calibration run (sequential
+gather of known bytes, same kernel, 16-B lane loads) -- on gfx950 FETCH_SIZE reads about 1/2
+of a wide coalesced stream's bytes (MI355X_MICROARCH.md, HBM).
+Writes profiles/gather_pmc.json (read by bench.py for roofline.traffic).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_kernel(path_glob, counter, kernel_re):
+    import re
+    vals = []
+    for path in glob.glob(path_glob, recursive=True):
+        for r in csv.DictReader(open(path)):
+            if r.get("Counter_Name") != counter:
+                continue
+            if re.search(kernel_re, r.get("Kernel_Name", "")):
+                vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def main(root):
+    table_re = r"k_gather<16, dgs::\(anonymous namespace\)::TableSrc>"
+    plain_re = r"k_gather<16, dgs::\(anonymous namespace\)::PlainSrc<long> >"
+    bf = per_kernel(f"{root}/pmc_bench_fetch/**/*counter_collection.csv", "FETCH_SIZE", table_re)
+    bw = per_kernel(f"{root}/pmc_bench_write/**/*counter_collection.csv", "WRITE_SIZE", table_re)
+    cf = per_kernel(f"{root}/pmc_calib_fetch/**/*counter_collection.csv", "FETCH_SIZE", plain_re)
+    cw = per_kernel(f"{root}/pmc_calib_write/**/*counter_collection.csv", "WRITE_SIZE", plain_re)
+    assert bf and bw and cf and cw, (len(bf), len(bw), len(cf), len(cw))
+    N, D = 1 << 22, 100
+    calib_read = N * (D * 4 + 8)          # rows + nids
+    calib_write = N * D * 4
+    cfetch = sorted(cf)[len(cf) // 2] * 1024
+    cwrite = sorted(cw)[len(cw) // 2] * 1024
+    read_factor = calib_read / cfetch
+    write_factor = calib_write / cwrite
+    bench_rows = float(os.environ.get("BENCH_ROWS_PER_LAUNCH", "0"))
+    fetch = sum(bf) / len(bf) * 1024 * read_factor
+    write = sum(bw) / len(bw) * 1024 * write_factor
+    out = {
+        "kernel": "k_gather<16, TableSrc>", "dim": D,
+        "calibration": {"workload": "sequential gather of 2^22 rows x 400 B (tools/gather_calib.py)",
+                        "expected_read_bytes": calib_read, "fetch_size_bytes": cfetch,
+                        "read_factor": read_factor, "expected_write_bytes": calib_write,
+                        "write_size_bytes": cwrite, "write_factor": write_factor},
+        "bench_launches": len(bf),
+        "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
+        "hbm_bytes_per_launch": fetch + write,
+        "rows_per_launch": bench_rows or None,
+        "hbm_bytes_per_row": (fetch + write) / bench_rows if bench_rows else None,
+    }
+    print(json.dumps(out, indent=1))
+    return out
+
+
+if __name__ == "__main__":
+    res = main(sys.argv[1])
+    if len(sys.argv) > 2:
+        json.dump(res, open(sys.argv[2], "w"), indent=1)
