@@ -86,8 +86,7 @@ def main():
     g2 = torch.Generator()
     g2.manual_seed(2)
     train = torch.randperm(N, generator=g2)[: N // 10]
-    per = (train.numel() + world - 1) // world
-    train_local = train[rank * per:(rank + 1) * per].to(dev)
+    train_local = seed_slice(train, rank, world).to(dev)
     log(f"[bench] graph N={N} E={E} d={args.dim} built in {time.time() - t0:.1f}s")
 
     # ---------------- services: whole graph + all features in HBM (configs[1])
@@ -144,16 +143,8 @@ def main():
 
     row_bytes = args.dim * 4
     gather_bytes = rows * (2 * row_bytes + 8)  # read row + write row + read nid
-    if dist:
-        t = torch.tensor([elapsed, float(edges), float(rows), float(gather_bytes),
-                          prof["gather_ms"]], dtype=torch.float64, device=dev)
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        elapsed = float(mx[0])
-        edges_all, rows_all, gbytes_all = float(t[1]), float(t[2]), float(t[3])
-    else:
-        edges_all, rows_all, gbytes_all = float(edges), float(rows), float(gather_bytes)
+    elapsed, edges_all, rows_all, gbytes_all = reduce_over_ranks(
+        dist, dev, elapsed, edges, rows, gather_bytes)
 
     # roofline of the dominant HBM kernel (feature gather), measured live with HIP events
     g_ms = prof["gather_ms"] / max(prof["gather_launches"], 1)
@@ -217,6 +208,25 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def reduce_over_ranks(dist, dev, elapsed, edges, rows, gather_bytes):
+    """Job time = max over ranks (every rank ran the same K steps between barriers); work =
+    sum over ranks.  dist is None for a single process."""
+    if dist is None:
+        return elapsed, float(edges), float(rows), float(gather_bytes)
+    t = torch.tensor([elapsed, float(edges), float(rows), float(gather_bytes)],
+                     dtype=torch.float64, device=dev)
+    mx = t.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(mx[0]), float(t[1]), float(t[2]), float(t[3])
+
+
+def seed_slice(train, rank, world):
+    """Train nids of this rank (node_classification.py:312-321: contiguous equal slices)."""
+    per = (train.numel() + world - 1) // world
+    return train[rank * per:(rank + 1) * per]
 
 
 def cpu_baseline(indptr, indices, feats, train, fan_out, args):

@@ -90,6 +90,11 @@ int dgs_set_nccl(int64_t nranks, const int64_t *unique_id, int64_t n_id, int64_t
   });
 }
 
+int dgs_set_host_comm(int64_t nranks, int64_t rank, dgs_host_allgather_fn allgather,
+                      dgs_host_barrier_fn barrier, void *ctx) {
+  return guard([&] { Comm::get().init_host((int)nranks, (int)rank, allgather, barrier, ctx); });
+}
+
 int dgs_get_local_rank(void) { return Comm::get().rank(); }
 int dgs_get_world_size(void) { return Comm::get().world(); }
 

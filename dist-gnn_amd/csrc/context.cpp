@@ -1,6 +1,7 @@
 // context.cpp -- launch-seed RNG, RCCL communicator, pointer utilities, profiler.
 #include "context.h"
 
+#include <algorithm>
 #include <cstring>
 
 #include "dgs_ops.h"
@@ -38,7 +39,23 @@ void Comm::init(int nranks, const void *unique_id, int rank) {
   DGS_HIP(hipMalloc(&dsizes_, sizeof(int64_t) * (kMaxDevices + 1)));
 }
 
+void Comm::init_host(int nranks, int rank, HostAllgatherFn ag, HostBarrierFn bar, void *ctx) {
+  DGS_CHECK(!initialized(), "communicator already initialised");
+  DGS_CHECK(nranks >= 1 && nranks <= kMaxDevices && rank >= 0 && rank < nranks,
+            "bad host communicator geometry");
+  DGS_CHECK(ag && bar, "host communicator needs allgather and barrier callbacks");
+  host_ag_ = ag;
+  host_bar_ = bar;
+  host_ctx_ = ctx;
+  world_ = nranks;
+  rank_ = rank;
+}
+
 void Comm::barrier() {
+  if (host_ag_) {
+    DGS_CHECK(host_bar_(host_ctx_) == 0, "host barrier failed");
+    return;
+  }
   if (!comm_) return;
   DGS_NCCL(ncclAllReduce(dbuf_, dbuf_, 1, ncclFloat, ncclSum, comm_, stream_));
   DGS_HIP(hipStreamSynchronize(stream_));
@@ -46,7 +63,13 @@ void Comm::barrier() {
 
 std::vector<int64_t> Comm::allgather_sizes(int64_t mine) {
   std::vector<int64_t> out(world_, mine);
-  if (!comm_ || world_ == 1) return out;
+  if (world_ == 1) return out;
+  if (host_ag_) {
+    DGS_CHECK(host_ag_(&mine, sizeof(int64_t), out.data(), host_ctx_) == 0,
+              "host allgather failed");
+    return out;
+  }
+  if (!comm_) return out;
   // device staging (the reference hands a host-registered vector to NCCL,
   // nccl_context.cc:61-77; RCCL gets device buffers here)
   DGS_HIP(hipMemcpyAsync(dsizes_ + kMaxDevices, &mine, sizeof(int64_t), hipMemcpyHostToDevice,
@@ -62,7 +85,20 @@ void Comm::allgather_bytes(const void *send, int64_t send_bytes, void *const *re
                            const int64_t *recv_bytes, hipStream_t st) {
   if (recv[rank_] != send && send_bytes > 0)
     DGS_HIP(hipMemcpyAsync(recv[rank_], send, send_bytes, hipMemcpyDeviceToDevice, st));
-  if (!comm_ || world_ == 1) return;
+  if (world_ == 1) return;
+  if (host_ag_) {
+    int64_t maxb = 1;
+    for (int i = 0; i < world_; ++i) maxb = std::max(maxb, recv_bytes[i]);
+    std::vector<char> hs(maxb, 0), hr((size_t)maxb * world_, 0);
+    DGS_HIP(hipStreamSynchronize(st));
+    if (send_bytes > 0) DGS_HIP(hipMemcpy(hs.data(), send, send_bytes, hipMemcpyDefault));
+    DGS_CHECK(host_ag_(hs.data(), maxb, hr.data(), host_ctx_) == 0, "host allgather failed");
+    for (int i = 0; i < world_; ++i)
+      if (i != rank_ && recv_bytes[i] > 0)
+        DGS_HIP(hipMemcpy(recv[i], hr.data() + (size_t)maxb * i, recv_bytes[i], hipMemcpyDefault));
+    return;
+  }
+  if (!comm_) return;
   DGS_HIP(hipStreamSynchronize(st));
   DGS_NCCL(ncclGroupStart());
   for (int i = 0; i < world_; ++i) {

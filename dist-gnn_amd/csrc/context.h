@@ -39,11 +39,18 @@ RandomEngine &rng();
 
 // RCCL communicator for the setup collectives (no collective runs in the sampling /
 // gather hot loop: remote rows are read one-sided through IPC-mapped peer memory).
+// Host transport for the setup collectives (tests, or ranks that share one device):
+// allgather(send[bytes] -> recv[world * bytes]) and barrier, both host memory.
+typedef int (*HostAllgatherFn)(const void *send, int64_t bytes, void *recv, void *ctx);
+typedef int (*HostBarrierFn)(void *ctx);
+
 class Comm {
  public:
   static Comm &get();
   void init(int nranks, const void *unique_id, int rank);
-  bool initialized() const { return comm_ != nullptr; }
+  void init_host(int nranks, int rank, HostAllgatherFn ag, HostBarrierFn bar, void *ctx);
+  bool initialized() const { return comm_ != nullptr || host_ag_ != nullptr; }
+  bool host_mode() const { return host_ag_ != nullptr; }
   int rank() const { return rank_; }
   int world() const { return world_; }
   void barrier();
@@ -57,6 +64,9 @@ class Comm {
 
  private:
   ncclComm_t comm_ = nullptr;
+  HostAllgatherFn host_ag_ = nullptr;
+  HostBarrierFn host_bar_ = nullptr;
+  void *host_ctx_ = nullptr;
   int rank_ = 0, world_ = 1;
   hipStream_t stream_ = nullptr;
   float *dbuf_ = nullptr;

@@ -34,6 +34,7 @@ _SIGS = {
     "dgs_version": (ctypes.c_char_p, []),
     "dgs_get_unique_id": (c_int, [p_i64]),
     "dgs_set_nccl": (c_int, [c_i64, p_i64, c_i64, c_i64]),
+    "dgs_set_host_comm": (c_int, [c_i64, c_i64, c_vp, c_vp, c_vp]),
     "dgs_get_local_rank": (c_int, []),
     "dgs_get_world_size": (c_int, []),
     "dgs_barrier": (c_int, []),

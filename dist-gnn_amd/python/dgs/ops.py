@@ -18,7 +18,7 @@ __all__ = [
     "_CAPI_cuda_sample_neighbors_bias", "_CAPI_cuda_sampled_tensor_relabel",
     "_CAPI_cuda_index_select", "_Test_Randn", "_Test_NCCLTensorAllGather",
     "_Test_GetLocalRank", "_Test_GetWorldSize", "_Test_ExtractEdgeData", "_Test_ExtractIndptr",
-    "_CAPI_set_random_seed",
+    "_CAPI_set_random_seed", "_CAPI_set_host_comm",
 ]
 
 _registered = {}
@@ -40,6 +40,44 @@ def _CAPI_set_nccl(nranks, unique_id_array, rank):
     """nccl_context.cc:20-45."""
     ids = i64_array(unique_id_array)
     check(lib.dgs_set_nccl(int(nranks), ids, len(unique_id_array), int(rank)))
+
+
+_HOST_AG = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                            ctypes.c_void_p)
+_HOST_BAR = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+_host_comm_refs = []
+
+
+def _CAPI_set_host_comm(group=None):
+    """ADDITIVE: run the library's setup collectives (IPC-handle / cache-list all-gathers,
+    barriers) over an existing torch.distributed group (e.g. gloo) instead of RCCL.  Used by the
+    multi-rank tests, where several ranks share one GPU; the hot path is unchanged."""
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+
+    def allgather(send, nbytes, recv, _ctx):
+        try:
+            src = torch.empty(nbytes, dtype=torch.uint8)
+            ctypes.memmove(src.data_ptr(), send, nbytes)
+            outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(outs, src, group=group)
+            for i, o in enumerate(outs):
+                ctypes.memmove(recv + i * nbytes, o.data_ptr(), nbytes)
+            return 0
+        except Exception:  # pragma: no cover - surfaced as a library error
+            return 1
+
+    def barrier(_ctx):
+        try:
+            dist.barrier(group)
+            return 0
+        except Exception:  # pragma: no cover
+            return 1
+
+    ag, bar = _HOST_AG(allgather), _HOST_BAR(barrier)
+    _host_comm_refs.extend([ag, bar])
+    check(lib.dgs_set_host_comm(world, rank, ctypes.cast(ag, ctypes.c_void_p),
+                                ctypes.cast(bar, ctypes.c_void_p), None))
 
 
 def _Test_GetLocalRank():

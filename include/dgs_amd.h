@@ -38,6 +38,14 @@ const char *dgs_version(void);
 int dgs_get_unique_id(int64_t *out_id16);
 /* replaces nccl::SetNCCL / NCCLContext::SetNCCL_ (nccl_context.cc:20-45; pybind.cc:51) */
 int dgs_set_nccl(int64_t nranks, const int64_t *unique_id, int64_t n_id, int64_t rank);
+/* ADDITIVE: host transport for the setup collectives instead of RCCL -- allgather(send[bytes]
+ * -> recv[world*bytes]) and barrier over host memory, supplied by the caller (e.g. over
+ * torch.distributed / gloo).  Lets ranks that share one GPU (tests) build P2P caches; the hot
+ * path is unchanged (one-sided device loads). */
+typedef int (*dgs_host_allgather_fn)(const void *send, int64_t bytes, void *recv, void *ctx);
+typedef int (*dgs_host_barrier_fn)(void *ctx);
+int dgs_set_host_comm(int64_t nranks, int64_t rank, dgs_host_allgather_fn allgather,
+                      dgs_host_barrier_fn barrier, void *ctx);
 /* replaces _Test_GetLocalRank / _Test_GetWorldSize (nccl_context.cc:31-32; pybind.cc:72-73).
  * Before dgs_set_nccl they report rank 0 of 1. */
 int dgs_get_local_rank(void);

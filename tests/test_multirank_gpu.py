@@ -1,0 +1,89 @@
+"""Two ranks sharing cuda:0 exercise the multi-rank path: IPC export / import of every cache
+block, cache-list all-gathers, node/feature tables with peer entries, one-sided peer reads.
+Results must equal the single-process oracle (P2P-cached output == uncached output)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def results():
+    world = 2
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as td:
+        procs = []
+        for r in range(world):
+            env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=str(port), LOCAL_RANK="0")
+            procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "mp_worker.py"),
+                                           os.path.join(td, f"r{r}.json")], env=env))
+        rcs = [p.wait(timeout=240) for p in procs]
+        assert rcs == [0] * world, rcs
+        return [json.load(open(os.path.join(td, f"r{r}.json"))) for r in range(world)]
+
+
+def test_world_and_allgather(results):
+    for r, res in enumerate(results):
+        assert res["world"] == 2 and res["local_rank"] == r
+        assert res["allgather"] == [[0.0, 0.0], [1.0, 1.0, 1.0]]
+
+
+def test_p2p_server_kat(results):
+    # tests/test_p2p_server.py: rank0 caches [0,3] -> [0,4,4]; rank1 [3,5] -> [0,0,5]
+    for res in results:
+        assert res["p2p_views"] == [[0, 4, 4], [0, 0, 5]]
+
+
+def test_feature_server_kat(results):
+    exp = [[float(x) for x in range(b, b + 10)] for b in (0, 30, 50, 70)]
+    for res in results:
+        assert res["feature_kat"] == exp
+
+
+def test_sharded_sampler_matches_oracle(results):
+    rng = np.random.default_rng(0)
+    n = 600
+    degs = rng.integers(0, 70, n)
+    degs[:4] = [0, 3000, 1500, 20]
+    ip = np.concatenate([[0], np.cumsum(degs)]).astype(np.int64)
+    ix = rng.integers(0, n, int(ip[-1])).astype(np.int64)
+    probs = (rng.random(ix.size) + 0.05).astype(np.float32)
+    for res in results:
+        for bias in (0, 1):
+            got = res[f"sample_bias{bias}"]
+            exp = O.node_classification_sample(np.array(got["seeds"]), ip, ix, [10, 5], False,
+                                               O.launch_seeds(777, 2),
+                                               probs=probs if bias else None)
+            for (gf, gr, gc), (_, ef, er, ec) in zip(got["hops"], exp):
+                assert gf == ef.tolist() and gr == er.tolist() and gc == ec.tolist()
+
+
+def test_cache_map_local_priority(results):
+    for r, res in enumerate(results):
+        key, idx, devid = res["map_bias0"]
+        assert key == list(range(600))
+        assert devid == [v % 2 for v in range(600)]
+        assert idx == [v // 2 for v in range(600)]
+
+
+def test_sharded_gather(results):
+    assert all(res["gather_ok"] for res in results)
