@@ -7,7 +7,9 @@ node_classification.py:219-229): P2PCacheSampler._CAPI_sample_node_classifiction
 ops._CAPI_cuda_index_select(labels, seeds), on a synthetic products-like RMAT graph (configs[1]:
 uniform sampler + full-feature gather, d = 100, whole graph in HBM).  Inputs are resident in HBM
 before the timed region.  N > 1 (torchrun): every rank holds the graph (replicated, weak
-scaling) and samples its own slice of the train nids; no collective runs in the timed loop.
+scaling, independent replicas) and samples its own slice of the train nids; no collective
+runs in the timed loop.  --shard caches node v on GPU v mod N instead (remote rows read
+one-sided over xGMI through IPC-mapped peer memory).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--scale S --ef E]
 """
@@ -44,6 +46,8 @@ def parse():
     p.add_argument("--dim", type=int, default=100)
     p.add_argument("--shard", action="store_true",
                    help="cache node v on GPU v %% N (P2P over xGMI) instead of replicating")
+    p.add_argument("--comm", choices=["gloo", "rccl"], default="gloo",
+                   help="transport of the library's setup collectives in --shard mode")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--seed", type=int, default=20261015)
@@ -55,17 +59,30 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # DGS_BENCH_SHARE_DEVICE=1 rehearses the N>1 flow on a 1-GPU box: every rank on cuda:0,
+    # gloo process group (RCCL refuses two ranks on one device).
+    share = os.environ.get("DGS_BENCH_SHARE_DEVICE") == "1"
+    if share:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     import dgs
     from DistGNN.dataloading import SeedGenerator
     from DistGNN.dataloading.synthetic import rmat_csc_torch
-    if world > 1:
-        from DistGNN.dist import create_communicator
-        create_communicator(world)
+    if world > 1 and args.shard:
+        # setup collectives only (IPC handles, cache lists); the timed loop has none
+        if args.comm == "rccl" and not share:
+            from DistGNN.dist import create_communicator
+            create_communicator(world)
+        else:
+            dgs.ops._CAPI_set_host_comm(dist.group.WORLD if share
+                                        else dist.new_group(backend="gloo"))
 
     fan_out = [int(x) for x in args.fan_out.split(",")]
     dev = torch.device("cuda", local_rank)
@@ -144,7 +161,7 @@ def main():
     row_bytes = args.dim * 4
     gather_bytes = rows * (2 * row_bytes + 8)  # read row + write row + read nid
     elapsed, edges_all, rows_all, gbytes_all = reduce_over_ranks(
-        dist, dev, elapsed, edges, rows, gather_bytes)
+        dist, torch.device("cpu") if share else dev, elapsed, edges, rows, gather_bytes)
 
     # roofline of the dominant HBM kernel (feature gather), measured live with HIP events
     g_ms = prof["gather_ms"] / max(prof["gather_launches"], 1)
@@ -205,6 +222,8 @@ def main():
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
+    del sampler, server  # collective destructors (sharded mode) before the group goes away
+    torch.cuda.synchronize()
     if dist:
         dist.barrier()
         dist.destroy_process_group()

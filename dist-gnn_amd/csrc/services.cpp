@@ -95,7 +95,9 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
   Comm &c = Comm::get();
   rank_ = c.rank();
   world_ = c.world();
-  DGS_CHECK(device_id == rank_ || c.host_mode(),
+  // sampler.cc:72.  Without a communicator every process is an independent replica (the
+  // reference would read an uninitialised rank); with the host transport ranks may share a GPU.
+  DGS_CHECK(device_id == rank_ || c.host_mode() || !c.initialized(),
             "device_id must equal the communicator rank (sampler.cc:72)");
   DGS_CHECK(num_nodes >= 0 && num_edges >= 0 && n_cache >= 0, "negative sizes");
   num_nodes_ = num_nodes;
@@ -263,7 +265,7 @@ FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_byt
   Comm &c = Comm::get();
   rank_ = c.rank();
   world_ = c.world();
-  DGS_CHECK(device_id == rank_ || c.host_mode(),
+  DGS_CHECK(device_id == rank_ || c.host_mode() || !c.initialized(),
             "device_id must equal the communicator rank (feature_server.cc:14)");
   num_rows_ = num_rows;
   row_bytes_ = row_bytes;
