@@ -115,6 +115,7 @@ def main():
     sampler = dgs.classes.P2PCacheSampler(indptr, indices, torch.Tensor(), cache, local_rank)
     server = dgs.classes.P2PCacheFeatureServer(feats, cache, local_rank)
     labels_dev = labels.to(dev)
+    layout = server._layout()
     torch.cuda.synchronize()
     log(f"[bench] services ready in {time.time() - t0:.1f}s")
     dgs.ops._CAPI_set_random_seed(args.seed + rank)
@@ -207,11 +208,14 @@ def main():
         "gather_GBps_wall": gbytes_all / elapsed / 1e9,
         "sampled_edges_per_step": edges_all / args.steps,
         "gathered_rows_per_step": rows_all / args.steps,
-        "sample_hops_ms_per_step": prof["sample_ms"] / args.steps,
+        "sample_span_ms_per_step": prof["sample_ms"] / args.steps,
         "gather_kernel_ms_per_step": prof["gather_ms"] / args.steps,
         "label_select_kernel_ms_per_step": prof["select_ms"] / args.steps,
         "roofline": {
-            "bound": "hbm", "kernel": "k_gather<16, TableSrc> (P2PCacheFeatureServer gather)",
+            "bound": "hbm",
+            "kernel": ("k_gather<16, StridedSrc> (P2PCacheFeatureServer gather, computed row "
+                       "addresses)" if layout >= 0 else
+                       "k_gather<16, TableSrc> (P2PCacheFeatureServer gather, address table)"),
             "timing": "hipExtLaunchKernelGGL start/stop events (GPU-side kernel start/end)",
             "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,

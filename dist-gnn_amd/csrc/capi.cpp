@@ -341,6 +341,10 @@ int dgs_feature_server_local_cache(const dgs_feature_server *s, const void **ptr
   });
 }
 
+int dgs_feature_server_layout(const dgs_feature_server *s, int *wshift) {
+  return guard([&] { *wshift = s->s->layout(); });
+}
+
 int dgs_feature_server_destroy(dgs_feature_server *s) {
   return guard([&] {
     delete s->s;

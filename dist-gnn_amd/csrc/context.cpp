@@ -225,7 +225,13 @@ void profile_collect() {
     if (!ev.b) continue;
     DGS_HIP(hipEventSynchronize(ev.b));
     float ms = 0;
-    DGS_HIP(hipEventElapsedTime(&ms, ev.a, ev.b));
+    // a span with no launch leaves its events unrecorded: nothing to count
+    if (hipEventElapsedTime(&ms, ev.a, ev.b) != hipSuccess) {
+      (void)hipGetLastError();
+      pool().push_back(ev.a);
+      pool().push_back(ev.b);
+      continue;
+    }
     if (ev.which == 0) {
       profiler().gather_ms += ms;
       profiler().gather_n += 1;

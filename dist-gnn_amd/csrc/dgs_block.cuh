@@ -59,4 +59,31 @@ __device__ __forceinline__ T block_sum(T v, T *lds) {
   return t;
 }
 
+// out[i] = carry + exclusive prefix of in[0..n) for one workgroup; each thread owns ITEMS
+// contiguous elements per pass (one block scan per THREADS * ITEMS elements).  Returns the
+// total.  `in` may be null (reads as zeros).  Call from every thread of the workgroup.
+template <int THREADS, int ITEMS, typename T>
+__device__ __forceinline__ T block_scan_range(const T *in, int64_t n, T *out, T *lds) {
+  T carry = T(0);
+  for (int64_t base = 0; base < n; base += (int64_t)THREADS * ITEMS) {
+    const int64_t b = base + (int64_t)threadIdx.x * ITEMS;
+    T v[ITEMS];
+    T s = T(0);
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      v[j] = (b + j < n) ? in[b + j] : T(0);
+      s += v[j];
+    }
+    T tot;
+    T ex = block_exclusive_scan<THREADS>(s, &tot, lds) + carry;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      if (b + j < n) out[b + j] = ex;
+      ex += v[j];
+    }
+    carry += tot;
+  }
+  return carry;
+}
+
 }  // namespace dgs

@@ -1,6 +1,8 @@
 // dgs_ops.h -- host-side launchers of the DGS-AMD HIP kernels (internal C++ interface).
 #pragma once
 
+#include <hip/hip_ext.h>
+
 #include "dgs_common.h"
 #include "dgs_table.cuh"
 
@@ -14,6 +16,14 @@ void gather_plain(const void *data, int64_t row_bytes, const void *nid, int nid_
 // address of every node's feature row.  align_or = OR of all row base addresses.
 void gather_table(const int64_t *ftab, uintptr_t align_or, int64_t row_bytes,
                   const int64_t *nids, int64_t n, void *out, hipStream_t st);
+// Strided cache layout (every node cached, node v at row v >> wshift of GPU v & (W - 1),
+// W = 1 << wshift <= 8; W = 1 is the whole-graph-in-HBM identity layout): the row address is
+// computed, so the gather reads no per-node table.  bases[d] = GPU d's (IPC-mapped) block.
+void gather_strided(const void *const *bases, int wshift, int64_t row_bytes,
+                    const int64_t *nids, int64_t n, void *out, hipStream_t st);
+// number of i < n with list[i] != start + i * stride (device count -> host)
+int64_t count_stride_mismatch(const int64_t *list, int64_t n, int64_t start, int64_t stride,
+                              hipStream_t st);
 // ftab[v] = base + v * row_bytes for v < n
 void ftab_init(int64_t *ftab, int64_t n, const void *base, int64_t row_bytes, hipStream_t st);
 // ftab[nids[i]] = base + i * row_bytes
@@ -81,9 +91,11 @@ Table relabel_table(HopScratch &ws, int64_t n_ub, hipStream_t st);
 
 // Relabel for the node-classification hop: mapping = cat(seeds[S], col[nnz]) where nnz is
 // read from d_nnz (device); writes unique ids to `unique` (first-occurrence order),
-// relabeled rows/cols to out_row/out_col (col may alias out_col), U to d_nunique.
+// relabeled rows/cols to out_row/out_col (col may alias out_col), U to d_nunique.  out_row
+// holds each edge's seed row r on entry (sample_hop's rowpos output) and is relabelled in
+// place; seeds_unique (every hop after the first) means label(r) == r and skips the lookup.
 void relabel_hop(const int64_t *seeds, Count S, const int64_t *col, const int64_t *d_nnz,
-                 int64_t nnz_cap, const int64_t *rowpos, const Table &table, int64_t *unique,
+                 int64_t nnz_cap, bool seeds_unique, const Table &table, int64_t *unique,
                  int64_t *out_row, int64_t *out_col, int64_t *d_nunique, HopScratch &ws,
                  hipStream_t st);
 
@@ -103,7 +115,7 @@ struct Profiler {
   int64_t gather_n = 0, sample_n = 0, select_n = 0;
 };
 Profiler &profiler();
-// which: 0 = feature-server gather kernel, 1 = sampling hop (events around the hop's
+// which: 0 = feature-server gather kernel, 1 = multi-hop sample call (span over all its
 // kernels), 2 = plain index_select gather kernel.
 // Kernel events: when profiling is on, returns (start, stop) events that hipExtLaunchKernelGGL
 // records at the kernel's own start / end; otherwise (null, null).
@@ -111,7 +123,9 @@ struct KernelEvents {
   hipEvent_t start = nullptr, stop = nullptr;
 };
 KernelEvents profile_kernel(int which);
-// Stream events around a group of launches (wall time of the group on the stream).
+// Stream events at both ends of a group of launches (one marker before the first and one
+// after the last kernel; used around a whole sample call, where the stream is idle anyway,
+// never between the kernels being measured).
 void profile_begin(hipStream_t st, int which);
 void profile_end(hipStream_t st, int which);
 void profile_collect();

@@ -8,9 +8,10 @@
 // every store instruction writes 64 * V contiguous bytes and every row read is a run of
 // contiguous 16-byte lane loads; no lane idles for row sizes that are not a multiple of the
 // wave width (d = 100 floats = 25 chunks).  Each thread keeps U independent row reads in
-// flight before its stores.  For the feature server the node -> (location, row) lookup is
-// fused into the same kernel (one 8-byte table load per row instead of a hash probe chain
-// plus a second pass).
+// flight before its stores, and the stores are non-temporal.  For the feature server the
+// node -> (location, row) lookup is fused into the same kernel: computed outright when every
+// node is cached in an identity / v-mod-W layout (StridedSrc), otherwise one 8-byte address
+// table load per row (TableSrc) instead of a hash probe chain plus a second pass.
 #include <hip/hip_ext.h>
 
 #include "dgs_common.h"
@@ -105,6 +106,32 @@ struct TableSrc {
   }
 };
 
+// Strided source (see gather_strided): loc = v & (W - 1), row = v >> wshift; the base is
+// picked with a select chain (a dynamically indexed kernel argument would go to scratch).
+template <bool Strided>
+struct StridedSrc {
+  const int64_t *nid;
+  const char *b0, *b1, *b2, *b3, *b4, *b5, *b6, *b7;
+  int64_t row_bytes;
+  int64_t row_base;
+  uint32_t wshift;
+  using Key = int64_t;
+  __device__ __forceinline__ Key key(uint32_t r) const { return nid[row_base + r]; }
+  __device__ __forceinline__ const char *addr(Key k) const {
+    if (!Strided) return b0 + k * row_bytes;
+    const uint32_t loc = (uint32_t)k & ((1u << wshift) - 1u);
+    const char *b = b0;
+    b = loc == 1 ? b1 : b;
+    b = loc == 2 ? b2 : b;
+    b = loc == 3 ? b3 : b;
+    b = loc == 4 ? b4 : b;
+    b = loc == 5 ? b5 : b;
+    b = loc == 6 ? b6 : b;
+    b = loc == 7 ? b7 : b;
+    return b + (k >> wshift) * row_bytes;
+  }
+};
+
 constexpr int kGatherThreads = 256;
 constexpr int kGatherUnroll = 4;
 
@@ -139,7 +166,9 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nch
 #pragma unroll
   for (int u = 0; u < kGatherUnroll; ++u) {
     const uint32_t g = base + u * kGatherThreads;
-    if (g < nchunks) *reinterpret_cast<T *>(out + (size_t)g * V) = v[u];
+    // non-temporal: the output is consumed by the next kernel, not re-read here, so it
+    // streams past L2 instead of evicting the rows other waves are fetching
+    if (g < nchunks) __builtin_nontemporal_store(v[u], reinterpret_cast<T *>(out + (size_t)g * V));
   }
 }
 
@@ -210,6 +239,53 @@ void gather_table(const int64_t *ftab, uintptr_t align_or, int64_t row_bytes,
   const int V = pick_vec(row_bytes, align_or | (uintptr_t)out);
   TableSrc s{ftab, nids, row_bytes, 0};
   launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0);
+}
+
+void gather_strided(const void *const *bases, int wshift, int64_t row_bytes,
+                    const int64_t *nids, int64_t n, void *out, hipStream_t st) {
+  if (n <= 0 || row_bytes <= 0) return;
+  DGS_CHECK(wshift >= 0 && wshift <= 3, "strided gather: at most 8 locations");
+  const int W = 1 << wshift;
+  const char *b[8];
+  uintptr_t align_or = (uintptr_t)out;
+  for (int d = 0; d < 8; ++d) {
+    b[d] = (const char *)bases[d < W ? d : 0];
+    align_or |= (uintptr_t)b[d];
+  }
+  const int V = pick_vec(row_bytes, align_or);
+  if (wshift == 0) {
+    StridedSrc<false> s{nids, b[0], b[1], b[2], b[3], b[4], b[5], b[6], b[7], row_bytes, 0, 0};
+    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0);
+  } else {
+    StridedSrc<true> s{nids, b[0], b[1], b[2], b[3], b[4], b[5], b[6], b[7], row_bytes, 0,
+                       (uint32_t)wshift};
+    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0);
+  }
+}
+
+namespace {
+__global__ void k_stride_mismatch(const int64_t *list, int64_t n, int64_t start, int64_t stride,
+                                  unsigned long long *bad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool miss = i < n && list[i] != start + i * stride;
+  const unsigned long long c = __popcll(__ballot(miss));
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(bad, c);
+}
+}  // namespace
+
+int64_t count_stride_mismatch(const int64_t *list, int64_t n, int64_t start, int64_t stride,
+                              hipStream_t st) {
+  if (n <= 0) return 0;
+  unsigned long long *bad = nullptr, h = 0;
+  DGS_HIP(hipMalloc(&bad, sizeof(*bad)));
+  DGS_HIP(hipMemsetAsync(bad, 0, sizeof(*bad), st));
+  hipLaunchKernelGGL(k_stride_mismatch, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, list,
+                     n, start, stride, bad);
+  DGS_LAUNCH_CHECK();
+  DGS_HIP(hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, st));
+  DGS_HIP(hipStreamSynchronize(st));
+  DGS_HIP(hipFree(bad));
+  return (int64_t)h;
 }
 
 void ftab_init(int64_t *ftab, int64_t n, const void *base, int64_t row_bytes, hipStream_t st) {

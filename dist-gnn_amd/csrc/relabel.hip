@@ -74,19 +74,21 @@ __global__ __launch_bounds__(kThreads) void k_scatter(const int64_t *a, Count na
   if (blockIdx.x == 0 && threadIdx.x == 0 && d_nunique) *d_nunique = boff[nblocks];
 }
 
-// Hop relabel: out_col[e] = lab(slot_of[na + e]), out_row[e] = lab(slot_of[rowpos[e]]);
-// then the touched slots are returned to empty.
+// Hop relabel: out_col[e] = lab(slot_of[na + e]); out_row[e] holds the seed row r of edge e
+// (written by the sampling kernel) and becomes lab(slot_of[r]) -- only needed when the seeds
+// may repeat (the first hop): later hops' seeds are the previous unique frontier, so seed r's
+// first occurrence is position r and its label is r.  Then the touched slots are emptied.
 __global__ __launch_bounds__(kThreads) void k_relabel_hop(Count nac, const int64_t *d_nb,
                                                           Table t, const uint32_t *slot_of,
-                                                          const int64_t *rowpos,
-                                                          int64_t *out_row, int64_t *out_col) {
+                                                          int remap_rows, int64_t *out_row,
+                                                          int64_t *out_col) {
   const int64_t na = nac.get();
   const int64_t nb = *d_nb;
   const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (e < nb) {
     const uint32_t sc = slot_of[na + e];
     out_col[e] = t.lab[sc];
-    out_row[e] = t.lab[slot_of[rowpos[e]]];
+    if (remap_rows) out_row[e] = t.lab[slot_of[out_row[e]]];
     t.key[sc] = kEmpty;
     t.val[sc] = kNoPos;
   }
@@ -150,7 +152,7 @@ Table relabel_table(HopScratch &ws, int64_t n_ub, hipStream_t st) {
 // (sample_hop with this Table); what is left is ranking the first occurrences and the COO
 // rewrite.
 void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64_t *d_nnz,
-                 int64_t nnz_cap, const int64_t *rowpos, const Table &t, int64_t *unique,
+                 int64_t nnz_cap, bool seeds_unique, const Table &t, int64_t *unique,
                  int64_t *out_row, int64_t *out_col, int64_t *d_nunique, HopScratch &ws,
                  hipStream_t st) {
   const int64_t n_ub = Sc.v + nnz_cap;
@@ -166,7 +168,7 @@ void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64
                      d_nnz, (int64_t)0, t, t.slot_of, boff, nblk, unique, d_nunique);
   DGS_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_relabel_hop, dim3((unsigned)nblk), dim3(kThreads), 0, st, Sc, d_nnz, t,
-                     t.slot_of, rowpos, out_row, out_col);
+                     t.slot_of, (int)!seeds_unique, out_row, out_col);
   DGS_LAUNCH_CHECK();
   ws.table_dirty = false;
 }

@@ -67,20 +67,24 @@ __device__ __forceinline__ int64_t row_count(int64_t deg, int64_t k, bool replac
   return replace ? (deg == 0 ? 0 : k) : (deg < k ? deg : k);
 }
 
-// Hub bookkeeping layout inside ws.hub (int64 words):
-//   [0] hub count, [1..] pad to 8, then hub_row[S], hub_nch[S + 1], hub_cptr[S + 1], hubid[S]
+// Hub bookkeeping.  `count` is one packed word, (hubs << 40) | chunks: a hub registers with a
+// single atomicAdd of (1 << 40) | its chunk count, which returns its index and its first chunk
+// together, so chunk offsets are increasing in the hub index with no prefix-sum pass.
+// Layout inside ws.hub (int64 words): [0..8) pad, hub_row[S], hub_cptr[S], hubid[S].
+constexpr int kHubShift = 40;
+constexpr uint64_t kHubChunkMask = (uint64_t(1) << kHubShift) - 1;
+constexpr int64_t kHubMaxRows = int64_t(1) << 23;  // hub index field: 24 bits
 struct HubView {
-  int64_t *count, *row, *nch, *cptr, *hubid;
+  int64_t *count, *row, *cptr, *hubid;
   __host__ __device__ static HubView make(int64_t *base, int64_t S) {
     HubView h;
     h.count = base;
     h.row = base + 8;
-    h.nch = h.row + S;
-    h.cptr = h.nch + S + 1;
-    h.hubid = h.cptr + S + 1;
+    h.cptr = h.row + S;
+    h.hubid = h.cptr + S;
     return h;
   }
-  static size_t bytes(int64_t S) { return sizeof(int64_t) * (size_t)(8 + 4 * S + 2); }
+  static size_t bytes(int64_t S) { return sizeof(int64_t) * (size_t)(8 + 3 * S); }
 };
 
 // ------------------------------------------------------------------------------------
@@ -111,9 +115,12 @@ __global__ __launch_bounds__(kTileRows) void k_prep(RowSrc src, const int64_t *_
     if (use_hubs) {
       int64_t h = -1;
       if (!replace && deg - k > kHubT) {
-        h = atomicAdd((unsigned long long *)hub.count, 1ull);
+        const uint64_t nch = (uint64_t)(deg - k + 511) / 512;
+        const uint64_t old = atomicAdd((unsigned long long *)hub.count,
+                                       (unsigned long long)((uint64_t(1) << kHubShift) | nch));
+        h = (int64_t)(old >> kHubShift);
         hub.row[h] = i;
-        hub.nch[h] = (deg - k + 511) / 512;
+        hub.cptr[h] = (int64_t)(old & kHubChunkMask);
         for (int64_t s2 = 0; s2 < k; ++s2) hubslot[h * k + s2] = (int32_t)s2;
       }
       hub.hubid[i] = h;
@@ -131,11 +138,10 @@ __global__ __launch_bounds__(kTileRows) void k_prep(RowSrc src, const int64_t *_
 }
 
 // Single workgroup: exclusive scan of tile sums (-> boff[0..nb], boff[nb] = nnz; the same for
-// the CDF sizes when biased-with-replacement) and the hub chunk prefix.
+// the CDF sizes when biased-with-replacement).
 __global__ __launch_bounds__(kScanThreads) void k_scan_hop(const int64_t *bsum,
                                                           const int64_t *tsum, Count Sc,
                                                           int64_t *boff, int64_t *tboff,
-                                                          int use_hubs, HubView hub,
                                                           int64_t *d_nnz, int64_t *d_cdf_total) {
   __shared__ int64_t lds[kScanThreads / 64];
   const int64_t nb = (Sc.get() + kTileRows - 1) / kTileRows;
@@ -143,32 +149,26 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_hop(const int64_t *bsum,
     const int64_t *in = pass ? tsum : bsum;
     int64_t *out = pass ? tboff : boff;
     if (!in) continue;
-    int64_t carry = 0;
-    for (int64_t base = 0; base < nb; base += kScanThreads) {
-      const int64_t i = base + threadIdx.x;
-      const int64_t v = i < nb ? in[i] : 0;
-      int64_t tot;
-      const int64_t ex = block_exclusive_scan<kScanThreads>(v, &tot, lds);
-      if (i < nb) out[i] = carry + ex;
-      carry += tot;
-    }
+    const int64_t tot = block_scan_range<kScanThreads, 4>(in, nb, out, lds);
     if (threadIdx.x == 0) {
-      out[nb] = carry;
-      *(pass ? d_cdf_total : d_nnz) = carry;
+      out[nb] = tot;
+      *(pass ? d_cdf_total : d_nnz) = tot;
     }
   }
-  if (!use_hubs) return;
-  const int64_t H = *hub.count;
-  int64_t carry = 0;
-  for (int64_t base = 0; base < H; base += kScanThreads) {
-    const int64_t i = base + threadIdx.x;
-    const int64_t v = i < H ? hub.nch[i] : 0;
-    int64_t tot;
-    const int64_t ex = block_exclusive_scan<kScanThreads>(v, &tot, lds);
-    if (i < H) hub.cptr[i] = carry + ex;
-    carry += tot;
-  }
-  if (threadIdx.x == 0) hub.cptr[H] = carry;
+}
+
+// x mod d, exact for 2^11 <= d < 2^30: the fp32 quotient estimate (relative error <= 2^-22,
+// so absolute error <= 2^32 / 2^11 * 2^-22 = 0.5) is within one of floor(x / d), and one
+// 32-bit multiply plus two corrections recover the remainder (the generic % spends four
+// quarter-rate multiplies).  Fuzzed against % over 2^34 pairs on gfx950.
+constexpr uint32_t kModBigMin = 2048;
+__device__ __forceinline__ uint32_t mod_big(uint32_t x, uint32_t d) {
+  const float rcp = __builtin_amdgcn_rcpf((float)d);
+  const uint32_t q = (uint32_t)((float)x * rcp);
+  int32_t r = (int32_t)(x - q * d);
+  r = r < 0 ? r + (int32_t)d : r;
+  r = r >= (int32_t)d ? r - (int32_t)d : r;
+  return (uint32_t)r;
 }
 
 // ------------------------------------------------------------------------------------
@@ -179,9 +179,10 @@ __global__ __launch_bounds__(256) void k_hub_reservoir(const RowInfo *__restrict
                                                        Count Sc, int64_t k, uint64_t seed,
                                                        HubView hub, int32_t *hubslot) {
   const int64_t S = Sc.get();
-  const int64_t H = *hub.count;
+  const uint64_t packed = (uint64_t)*hub.count;
+  const int64_t H = (int64_t)(packed >> kHubShift);
   if (H == 0) return;
-  const int64_t total = hub.cptr[H];
+  const int64_t total = (int64_t)(packed & kHubChunkMask);
   const int lane = threadIdx.x & 63;
   // Each wave owns one contiguous range of chunks: one binary search per wave, then the hub
   // index only moves forward (a dependent search per chunk would dominate the Philox work).
@@ -195,14 +196,14 @@ __global__ __launch_bounds__(256) void k_hub_reservoir(const RowInfo *__restrict
     if (hub.cptr[mid] <= c0) lo = mid; else hi = mid;
   }
   int64_t h = lo;
-  int64_t hstart = hub.cptr[h], hnext = hub.cptr[h + 1];
+  int64_t hstart = hub.cptr[h], hnext = h + 1 < H ? hub.cptr[h + 1] : total;
   int64_t r = hub.row[h];
   int64_t deg = ri_deg(rowinfo[r]);
   for (int64_t c = c0; c < c1; ++c) {
     while (c >= hnext) {
       ++h;
       hstart = hnext;
-      hnext = hub.cptr[h + 1];
+      hnext = h + 1 < H ? hub.cptr[h + 1] : total;
       r = hub.row[h];
       deg = ri_deg(rowinfo[r]);
     }
@@ -214,16 +215,33 @@ __global__ __launch_bounds__(256) void k_hub_reservoir(const RowInfo *__restrict
         make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)lane, 0u), kk);
     const uint4 o4b = philox4x32_10(
         make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)(lane + 64), 0u), kk);
+    // every d = idx + 1 of this chunk is >= k + 512 q + 1 (wave-uniform test)
+    if (k + 512 * q + 1 >= (int64_t)kModBigMin && deg < (int64_t(1) << 30)) {
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const uint4 o4 = tt ? o4b : o4a;
-      const int64_t base = k + lane + 64 * tt + 512 * q;
+      for (int tt = 0; tt < 2; ++tt) {
+        const uint4 o4 = tt ? o4b : o4a;
+        const int64_t base = k + lane + 64 * tt + 512 * q;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const int64_t idx = base + 128 * w;
-        if (idx < deg) {
-          const uint32_t num = u4_get(o4, w) % (uint32_t)(idx + 1);
-          if ((int64_t)num < k) atomicMax(sl + num, (int32_t)idx);
+        for (int w = 0; w < 4; ++w) {
+          const int64_t idx = base + 128 * w;
+          if (idx < deg) {
+            const uint32_t num = mod_big(u4_get(o4, w), (uint32_t)(idx + 1));
+            if ((int64_t)num < k) atomicMax(sl + num, (int32_t)idx);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const uint4 o4 = tt ? o4b : o4a;
+        const int64_t base = k + lane + 64 * tt + 512 * q;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const int64_t idx = base + 128 * w;
+          if (idx < deg) {
+            const uint32_t num = u4_get(o4, w) % (uint32_t)(idx + 1);
+            if ((int64_t)num < k) atomicMax(sl + num, (int32_t)idx);
+          }
         }
       }
     }
@@ -537,7 +555,7 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     DGS_HIP(hipMemsetAsync(d_nnz, 0, sizeof(int64_t), st));
     return;
   }
-  const bool use_hubs = !bias && !replace && k > 0;
+  const bool use_hubs = !bias && !replace && k > 0 && S < kHubMaxRows;
   // the hub counter lives in its own buffer: zeroed at allocation, then reset on the device by
   // every hop that used it
   if (ws.hubcount.ensure(64)) DGS_HIP(hipMemsetAsync(ws.hubcount.p, 0, 64, st));
@@ -549,19 +567,17 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   int32_t *tpre = ws.tpre.as<int32_t>();
   int32_t *tpre2 = tpre + S;
   if (use_hubs) ws.hubslot.ensure(sizeof(int32_t) * (size_t)(S * k));
-  profile_begin(st, 1);
   hipLaunchKernelGGL(k_prep, dim3((unsigned)nb), dim3(kTileRows), 0, st, src, seeds, Sc, k,
                      (int)replace, (int)use_hubs, (int)bias_replace, rowinfo, tpre, tpre2, bsum,
                      tsum, hub, ws.hubslot.as<int32_t>(), table);
   DGS_LAUNCH_CHECK();
   if (k == 0) {  // seeds still enter the relabel table (frontier = unique(seeds))
     DGS_HIP(hipMemsetAsync(d_nnz, 0, sizeof(int64_t), st));
-    profile_end(st, 1);
     return;
   }
   hipLaunchKernelGGL(k_scan_hop, dim3(1), dim3(kScanThreads), 0, st, bsum,
-                     bias_replace ? (const int64_t *)tsum : nullptr, Sc, boff, tboff,
-                     (int)use_hubs, hub, d_nnz, bsum + 2 * nb + 1);
+                     bias_replace ? (const int64_t *)tsum : nullptr, Sc, boff, tboff, d_nnz,
+                     bsum + 2 * nb + 1);
   DGS_LAUNCH_CHECK();
 
   if (!bias) {
@@ -601,7 +617,6 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     }
     DGS_LAUNCH_CHECK();
   }
-  profile_end(st, 1);
 }
 
 }  // namespace dgs

@@ -16,16 +16,8 @@ constexpr int kTile = kTileThreads * kTileItems;
 __global__ __launch_bounds__(kScanThreads) void k_scan_small(const int64_t *in, int64_t n,
                                                              int64_t *out) {
   __shared__ int64_t lds[kScanThreads / 64];
-  int64_t carry = 0;
-  for (int64_t base = 0; base < n; base += kScanThreads) {
-    const int64_t i = base + threadIdx.x;
-    const int64_t v = i < n ? in[i] : 0;
-    int64_t tot;
-    const int64_t ex = block_exclusive_scan<kScanThreads>(v, &tot, lds);
-    if (i < n) out[i] = carry + ex;
-    carry += tot;
-  }
-  if (threadIdx.x == 0) out[n] = carry;
+  const int64_t tot = block_scan_range<kScanThreads, 8>(in, n, out, lds);
+  if (threadIdx.x == 0) out[n] = tot;
 }
 
 __global__ __launch_bounds__(kTileThreads) void k_tile_reduce(const int64_t *in, int64_t n,

@@ -191,11 +191,9 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
   int64_t *hsz = sizes_host_.as<int64_t>();
   std::vector<int64_t> fcap(L), ecap(L);
   bounds(n_seeds, fan_out, L, fcap.data(), ecap.data());
-  int64_t max_e = 1;
-  for (int h = 0; h < L; ++h) max_e = std::max(max_e, ecap[h]);
-  rowpos_.ensure(sizeof(int64_t) * (size_t)max_e);
   const int64_t *cur = seeds;
   Count S{n_seeds, nullptr};
+  profile_begin(st, 1);
   for (int h = 0; h < L; ++h) {
     const int64_t k = fan_out[L - 1 - h];
     DGS_CHECK(k >= 0, "fan_out entries must be non-negative");
@@ -205,13 +203,14 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
     int64_t *d_uniq = dsz + 3 * h + 1;
     const Table t = relabel_table(ws_, S.v + nnz_cap, st);
     ws_.table_dirty = true;
-    sample_hop(src_, cur, S, k, replace, bias_, seed, rowpos_.as<int64_t>(), cols[h], d_nnz, t,
-               ws_, st);
-    relabel_hop(cur, S, cols[h], d_nnz, nnz_cap, rowpos_.as<int64_t>(), t, frontiers[h], rows[h],
-                cols[h], d_uniq, ws_, st);
+    // rows[h] receives each edge's seed row r from the sampler and is relabelled in place
+    sample_hop(src_, cur, S, k, replace, bias_, seed, rows[h], cols[h], d_nnz, t, ws_, st);
+    relabel_hop(cur, S, cols[h], d_nnz, nnz_cap, /*seeds_unique=*/h > 0, t, frontiers[h],
+                rows[h], cols[h], d_uniq, ws_, st);
     cur = frontiers[h];
     S = Count{fcap[h], d_uniq};
   }
+  profile_end(st, 1);
   DGS_HIP(hipMemcpyAsync(hsz, dsz, sizeof(int64_t) * (size_t)(3 * L), hipMemcpyDeviceToHost, st));
   DGS_HIP(hipStreamSynchronize(st));
   int64_t s = n_seeds;
@@ -296,15 +295,44 @@ FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_byt
     align_or_ |= (uintptr_t)feat_srv_->ptr(d);
   }
   DGS_HIP(hipStreamSynchronize(st));
+  detect_strided(lists, nbytes, st);
   if (world_ > 1)
     for (void *p : lists) DGS_HIP(hipFree(p));
   DGS_HIP(hipFree(nids));
 }
 
+// Whole graph cached in a computable layout: the local list is arange(N) (local priority makes
+// every read local), or GPU d holds arange(d, N, W) for a power-of-two W (the v mod W shard).
+void FeatureServer::detect_strided(const std::vector<void *> &lists,
+                                   const std::vector<int64_t> &nbytes, hipStream_t st) {
+  const int64_t N = num_rows_;
+  if (N <= 0) return;
+  if (nbytes[rank_] / 8 == N &&
+      count_stride_mismatch((const int64_t *)lists[rank_], N, 0, 1, st) == 0) {
+    wshift_ = 0;
+    for (int d = 0; d < kMaxDevices; ++d) bases_[d] = feat_srv_->ptr(rank_);
+    return;
+  }
+  const int W = world_;
+  if (W < 2 || (W & (W - 1)) != 0) return;
+  for (int d = 0; d < W; ++d) {
+    const int64_t want = N > d ? (N - d + W - 1) / W : 0;
+    if (nbytes[d] / 8 != want) return;
+    if (count_stride_mismatch((const int64_t *)lists[d], want, d, W, st) != 0) return;
+  }
+  int sh = 0;
+  while ((1 << sh) < W) ++sh;
+  for (int d = 0; d < kMaxDevices; ++d) bases_[d] = feat_srv_->ptr(d < W ? d : 0);
+  wshift_ = sh;
+}
+
 FeatureServer::~FeatureServer() { delete feat_srv_; }
 
 void FeatureServer::gather(const int64_t *nids, int64_t n, void *out, hipStream_t st) const {
-  gather_table(ftab_.as<int64_t>(), align_or_, row_bytes_, nids, n, out, st);
+  if (wshift_ >= 0)
+    gather_strided(bases_, wshift_, row_bytes_, nids, n, out, st);
+  else
+    gather_table(ftab_.as<int64_t>(), align_or_, row_bytes_, nids, n, out, st);
 }
 
 }  // namespace dgs

@@ -82,7 +82,7 @@ class Sampler {
   DevBuf ntab_;
   RowSrc src_{};
   HopScratch ws_;
-  DevBuf rowpos_, sizes_;
+  DevBuf sizes_;
   HostPinned sizes_host_;
 };
 
@@ -94,14 +94,20 @@ class FeatureServer {
   void gather(const int64_t *nids, int64_t n, void *out, hipStream_t st) const;
   const void *local() const { return feat_srv_ ? feat_srv_->local() : nullptr; }
   int64_t local_rows() const { return feat_srv_ ? feat_srv_->items(rank_) : 0; }
+  int layout() const { return wshift_; }
 
  private:
   int64_t num_rows_ = 0, row_bytes_ = 0;
   int rank_ = 0, world_ = 1;
   HostView h_data_;
   P2PServer *feat_srv_ = nullptr;
+  void detect_strided(const std::vector<void *> &lists, const std::vector<int64_t> &nbytes,
+                      hipStream_t st);
   DevBuf ftab_;
   uintptr_t align_or_ = 0;
+  // >= 0: every node is cached in the strided layout of gather_strided (no ftab reads)
+  int wshift_ = -1;
+  const void *bases_[kMaxDevices] = {};
 };
 
 }  // namespace dgs

@@ -66,6 +66,7 @@ _SIGS = {
     "dgs_feature_server_create": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, p_vp]),
     "dgs_feature_server_gather": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "dgs_feature_server_local_cache": (c_int, [c_vp, p_vp, p_i64]),
+    "dgs_feature_server_layout": (c_int, [c_vp, ctypes.POINTER(c_int)]),
     "dgs_feature_server_destroy": (c_int, [c_vp]),
     "dgs_profile_enable": (c_int, [c_int]),
     "dgs_profile_read": (c_int, [ctypes.POINTER(c_dbl), p_i64, ctypes.POINTER(c_dbl), p_i64,

@@ -53,6 +53,17 @@ class TensorP2PServer:
             self._h = None
 
 
+def plan_ptrs(base, caps):
+    """Pointer arrays of the per-hop (frontier, row, col) buffers laid out back to back."""
+    fr_p, row_p, col_p, off = [], [], [], 0
+    for f, e in caps:
+        fr_p.append(base + 8 * off)
+        row_p.append(base + 8 * (off + f))
+        col_p.append(base + 8 * (off + f + e))
+        off += f + 2 * e
+    return vp_array(fr_p), vp_array(row_p), vp_array(col_p)
+
+
 class P2PCacheSampler:
     """sampler.{h,cc}: multi-hop node-classification sampler over a host CSC graph with a
     GPU-cached sub-CSR (local / peer GPUs) for `cache_nids`."""
@@ -103,26 +114,27 @@ class P2PCacheSampler:
         fo, caps, total = plan
         # one allocation for every hop's (frontier, row, col) buffers
         buf = torch.empty(max(total, 1), dtype=torch.int64, device=s.device)
-        base, off = buf.data_ptr(), 0
-        fr_p, row_p, col_p, views = [], [], [], []
-        for f, e in caps:
-            views.append((off, f, off + f, e, off + f + e))
-            fr_p.append(base + 8 * off)
-            row_p.append(base + 8 * (off + f))
-            col_p.append(base + 8 * (off + f + e))
-            off += f + 2 * e
+        base = buf.data_ptr()
+        fr_p, row_p, col_p = plan_ptrs(base, caps)
         sizes = (c_i64 * (3 * L))()
         check(lib.dgs_sampler_sample(self._h, c_vp(s.data_ptr()), s.numel(), fo, L,
-                                     int(bool(replace)), vp_array(fr_p), vp_array(row_p),
-                                     vp_array(col_p), sizes, stream_ptr(s.device)))
+                                     int(bool(replace)), fr_p, row_p, col_p, sizes,
+                                     stream_ptr(s.device)))
+        # all views in one split: [U_h, pad, nnz_h, pad, nnz_h, pad] per hop
+        lens = []
+        for h, (f, e) in enumerate(caps):
+            U, nnz = sizes[3 * h + 1], sizes[3 * h + 2]
+            lens += (U, f - U, nnz, e - nnz, nnz, e - nnz)
+        if total == 0:
+            lens.append(1)
+        else:
+            lens.append(buf.numel() - total)
+        parts = buf.split(lens)
         out = []
         cur = seeds
         cast = self._id_dtype != torch.int64
-        for h, (fo_off, _, ro_off, e, co_off) in enumerate(views):
-            U, nnz = sizes[3 * h + 1], sizes[3 * h + 2]
-            fr = buf[fo_off:fo_off + U]
-            r = buf[ro_off:ro_off + nnz]
-            c = buf[co_off:co_off + nnz]
+        for h in range(L):
+            fr, r, c = parts[6 * h], parts[6 * h + 2], parts[6 * h + 4]
             if cast:
                 fr, r, c = fr.to(self._id_dtype), r.to(self._id_dtype), c.to(self._id_dtype)
             out.append((cur, fr, r, c))
@@ -204,6 +216,12 @@ class P2PCacheFeatureServer:
         check(lib.dgs_feature_server_gather(self._h, c_vp(n.data_ptr()), n.numel(),
                                             c_vp(out.data_ptr()), stream_ptr(n.device)))
         return out
+
+    def _layout(self):
+        """ADDITIVE: -1 = address-table gather, w >= 0 = strided layout over 2^w GPUs."""
+        w = ctypes.c_int()
+        check(lib.dgs_feature_server_layout(self._h, ctypes.byref(w)))
+        return w.value
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -171,6 +171,10 @@ int dgs_feature_server_gather(dgs_feature_server *s, const int64_t *nids, int64_
                               void *out, void *stream);
 int dgs_feature_server_local_cache(const dgs_feature_server *s, const void **ptr,
                                    int64_t *rows);
+/* ADDITIVE.  Address layout the gather uses: -1 = per-node address table (general cache
+ * placement), w >= 0 = every node cached in the strided layout (node v at row v >> w of GPU
+ * v & (2^w - 1); w = 0 is the whole-graph-in-HBM identity), no per-node table read. */
+int dgs_feature_server_layout(const dgs_feature_server *s, int *wshift);
 int dgs_feature_server_destroy(dgs_feature_server *s);
 
 /* ------------------------------------------------------------------------------------

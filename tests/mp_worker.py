@@ -64,6 +64,7 @@ def main(out_path):
     q = rng.integers(0, n, 500)
     got = fs2._CAPI_get_feature(torch.from_numpy(q).cuda()).cpu().numpy()
     res["gather_ok"] = bool(np.array_equal(got, data[q]))
+    res["gather_layout"] = fs2._layout()
     torch.cuda.synchronize()
     del fs, fs2, srv
     dist.barrier()

@@ -27,13 +27,16 @@ def _gold():
     return np.load(os.path.join(GOLD, "sampler_golden.npz"))
 
 
-def _hub_graph(seed=0):
-    """Small graph with degree-0 rows, deg == k rows and hub rows (deg >> 1024 + k)."""
+def _hub_graph(seed=0, giant=True):
+    """Small graph with degree-0 rows, deg == k rows and hub rows (deg >> 1024 + k).
+    giant=False drops the 250K-degree row (float-atomic heat sums over it are order
+    dependent beyond the 1e-5 tolerance, preprocess_heat.cu uses atomicAdd too)."""
     rng = np.random.default_rng(seed)
     n = 400
     degs = rng.integers(0, 80, n)
     degs[:6] = [0, 1, 5, 15, 3000, 9000]
     degs[6:10] = [130, 512, 1040, 1100]
+    degs[10:12] = [2600, 250000 if giant else 2700]  # hub chunks on both modulo paths
     indptr = np.concatenate([[0], np.cumsum(degs)]).astype(np.int64)
     indices = rng.integers(0, n, int(indptr[-1])).astype(np.int64)
     probs = (rng.random(indices.size) + 0.01).astype(np.float32)
@@ -244,11 +247,26 @@ def test_sampler_getters(dgs):
 def test_feature_server_matches_oracle(dgs):
     rng = np.random.default_rng(9)
     data = rng.standard_normal((3000, 100)).astype(np.float32)
-    for cnids in (np.arange(3000), rng.permutation(3000)[:1000], np.array([7])):
+    for cnids, layout in ((np.arange(3000), 0), (rng.permutation(3000)[:1000], -1),
+                          (np.array([7]), -1), (rng.permutation(3000), -1)):
         fs = dgs.classes.P2PCacheFeatureServer(torch.from_numpy(data), torch.from_numpy(cnids), 0)
+        assert fs._layout() == layout  # identity layout -> computed addresses, no table
         q = rng.integers(0, 3000, 4096)
         got = fs._CAPI_get_feature(_cuda(q))
         assert np.array_equal(got.cpu().numpy(), O.index_select(data, q))
+
+
+@pytest.mark.parametrize("dim,dtype", [(33, np.float32), (1, np.int64), (3, np.int16),
+                                       (128, np.float32), (7, np.uint8)])
+def test_feature_server_row_sizes(dgs, dim, dtype):
+    """Every vector width of the gather (16/8/4/2/1-byte chunks), both address layouts."""
+    rng = np.random.default_rng(dim)
+    data = (rng.standard_normal((777, dim)) * 100).astype(dtype)
+    for cnids in (np.arange(777), rng.permutation(777)[:300]):
+        fs = dgs.classes.P2PCacheFeatureServer(torch.from_numpy(data), torch.from_numpy(cnids), 0)
+        q = np.concatenate([rng.integers(0, 777, 999), [0, 776]])
+        got = fs._CAPI_get_feature(_cuda(q)).cpu().numpy()
+        assert np.array_equal(got, data[q])
 
 
 def test_tensor_p2p_server_local(dgs):
@@ -261,7 +279,7 @@ def test_tensor_p2p_server_local(dgs):
 # ------------------------------------------------------------------ heat
 @pytest.mark.parametrize("bias", [False, True])
 def test_heat_matches_oracle(dgs, bias):
-    indptr, indices, probs = _hub_graph(2)
+    indptr, indices, probs = _hub_graph(2, giant=False)
     probs = probs + np.float32(0.05)
     n = indptr.size - 1
     heat = np.random.default_rng(1).random(n).astype(np.float32)
@@ -277,7 +295,7 @@ def test_heat_matches_oracle(dgs, bias):
 
 
 def test_heat_uva_host_graph(dgs):
-    indptr, indices, _ = _hub_graph(4)
+    indptr, indices, _ = _hub_graph(4, giant=False)
     n = indptr.size - 1
     ip, ix = torch.from_numpy(indptr), torch.from_numpy(indices)
     dgs.ops._CAPI_tensor_pin_memory(ip)

@@ -87,3 +87,5 @@ def test_cache_map_local_priority(results):
 
 def test_sharded_gather(results):
     assert all(res["gather_ok"] for res in results)
+    # v mod 2 shard -> strided layout (peer rows through the IPC-mapped block, no table)
+    assert all(res["gather_layout"] == 1 for res in results)
