@@ -353,10 +353,14 @@ int dgs_feature_server_destroy(dgs_feature_server *s) {
 }
 
 // ------------------------------------------------------------------ profiling
-int dgs_profile_enable(int on) {
+int dgs_profile_enable(int mask) {
   return guard([&] {
     profile_collect();
-    profiler().on = on != 0;
+    // which-index bits: 0 = gather, 1 = sample, 2 = select (dgs_ops.h)
+    int m = mask & 7;
+    if (mask != 0 && (mask & ~7) != 0) m = 7;
+    profiler().mask = m;
+    profiler().on = m != 0;
   });
 }
 

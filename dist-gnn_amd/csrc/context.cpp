@@ -193,7 +193,7 @@ Profiler &profiler() {
 
 KernelEvents profile_kernel(int which) {
   KernelEvents ev;
-  if (!profiler().on) return ev;
+  if (!profiler().wants(which)) return ev;
   ev.start = take_event();
   ev.stop = take_event();
   pending().push_back(EvPair{ev.start, ev.stop, which});
@@ -201,14 +201,14 @@ KernelEvents profile_kernel(int which) {
 }
 
 void profile_begin(hipStream_t st, int which) {
-  if (!profiler().on) return;
+  if (!profiler().wants(which)) return;
   EvPair ev{take_event(), nullptr, which};
   DGS_HIP(hipEventRecord(ev.a, st));
   pending().push_back(ev);
 }
 
 void profile_end(hipStream_t st, int which) {
-  if (!profiler().on) return;
+  if (!profiler().wants(which)) return;
   auto &pv = pending();
   for (auto it = pv.rbegin(); it != pv.rend(); ++it) {
     if (it->which == which && it->b == nullptr) {

@@ -63,19 +63,30 @@ struct DevBuf {
 struct HostPinned {
   void *p = nullptr;
   size_t bytes = 0;
+  unsigned flags = hipHostMallocDefault;
   ~HostPinned() {
     if (p) (void)hipHostFree(p);
   }
   void ensure(size_t need) {
     if (need <= bytes && p) return;
     if (p) (void)hipHostFree(p);
-    DGS_HIP(hipHostMalloc(&p, need, hipHostMallocDefault));
+    DGS_HIP(hipHostMalloc(&p, need, flags));
     bytes = need;
   }
   template <typename T>
   T *as() const {
     return reinterpret_cast<T *>(p);
   }
+};
+
+// Sizes a kernel publishes to the host without a copy or a stream synchronisation: `n` device
+// words are written to coherent pinned host memory host[1..n], then host[0] = seq with a
+// system-scope release (HostSizes{} = nothing to publish).
+struct HostSizes {
+  const int64_t *dev = nullptr;
+  int64_t n = 0;
+  int64_t *host = nullptr;  // device-visible address of the pinned block
+  uint64_t seq = 0;
 };
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

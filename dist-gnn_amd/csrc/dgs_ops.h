@@ -97,7 +97,7 @@ Table relabel_table(HopScratch &ws, int64_t n_ub, hipStream_t st);
 void relabel_hop(const int64_t *seeds, Count S, const int64_t *col, const int64_t *d_nnz,
                  int64_t nnz_cap, bool seeds_unique, const Table &table, int64_t *unique,
                  int64_t *out_row, int64_t *out_col, int64_t *d_nunique, HopScratch &ws,
-                 hipStream_t st);
+                 hipStream_t st, const HostSizes &pub = HostSizes{});
 
 // Generic relabel (TensorRelabelCUDA): mapping[nm], req[nr] -> unique, relabeled req (-1 if
 // absent), d_nunique.
@@ -111,12 +111,14 @@ void take_i64(const int64_t *src, const int64_t *idx, int64_t n, int64_t *out, h
 // ---------------------------------------------------------------- profiling
 struct Profiler {
   bool on = false;
+  int mask = 0;  // bit `which` enables that measurement
+  bool wants(int which) const { return on && ((mask >> which) & 1); }
   double gather_ms = 0, sample_ms = 0, select_ms = 0;
   int64_t gather_n = 0, sample_n = 0, select_n = 0;
 };
 Profiler &profiler();
-// which: 0 = feature-server gather kernel, 1 = multi-hop sample call (span over all its
-// kernels), 2 = plain index_select gather kernel.
+// which: 0 = feature-server gather kernel, 1 = multi-hop sample call (events before its
+// first and after its last kernel), 2 = plain index_select gather kernel.
 // Kernel events: when profiling is on, returns (start, stop) events that hipExtLaunchKernelGGL
 // records at the kernel's own start / end; otherwise (null, null).
 struct KernelEvents {

@@ -53,7 +53,8 @@ __global__ __launch_bounds__(kThreads) void k_scatter(const int64_t *a, Count na
                                                       int64_t nb_fixed, Table t,
                                                       const uint32_t *slot_of,
                                                       const int64_t *boff, int64_t nblocks,
-                                                      int64_t *unique, int64_t *d_nunique) {
+                                                      int64_t *unique, int64_t *d_nunique,
+                                                      HostSizes pub) {
   __shared__ int64_t lds[kThreads / 64];
   const int64_t na = nac.get();
   const int64_t n = na + (d_nb ? *d_nb : nb_fixed);
@@ -71,7 +72,18 @@ __global__ __launch_bounds__(kThreads) void k_scatter(const int64_t *a, Count na
     unique[pos] = elem(a, na, b, i);
     t.lab[sl] = (int32_t)pos;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && d_nunique) *d_nunique = boff[nblocks];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (d_nunique) *d_nunique = boff[nblocks];
+    if (pub.host) {
+      // every size of the call is final here (earlier hops' by earlier kernels, this hop's U
+      // just above): publish them so the host need not wait for the relabel pass
+      for (int64_t j = 0; j < pub.n; ++j)
+        __hip_atomic_store(pub.host + 1 + j, pub.dev[j], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(pub.host, (int64_t)pub.seq, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // Hop relabel: out_col[e] = lab(slot_of[na + e]); out_row[e] holds the seed row r of edge e
@@ -154,7 +166,7 @@ Table relabel_table(HopScratch &ws, int64_t n_ub, hipStream_t st) {
 void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64_t *d_nnz,
                  int64_t nnz_cap, bool seeds_unique, const Table &t, int64_t *unique,
                  int64_t *out_row, int64_t *out_col, int64_t *d_nunique, HopScratch &ws,
-                 hipStream_t st) {
+                 hipStream_t st, const HostSizes &pub) {
   const int64_t n_ub = Sc.v + nnz_cap;
   const int64_t nblk = ceil_div(n_ub > 0 ? n_ub : 1, kThreads);
   ws.misc.ensure(sizeof(int64_t) * (size_t)(2 * nblk + 2));
@@ -165,7 +177,7 @@ void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64
   DGS_LAUNCH_CHECK();
   scan_small(bcnt, nblk, boff, st);
   hipLaunchKernelGGL(k_scatter, dim3((unsigned)nblk), dim3(kThreads), 0, st, seeds, Sc, col,
-                     d_nnz, (int64_t)0, t, t.slot_of, boff, nblk, unique, d_nunique);
+                     d_nnz, (int64_t)0, t, t.slot_of, boff, nblk, unique, d_nunique, pub);
   DGS_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_relabel_hop, dim3((unsigned)nblk), dim3(kThreads), 0, st, Sc, d_nnz, t,
                      t.slot_of, (int)!seeds_unique, out_row, out_col);
@@ -192,7 +204,7 @@ void relabel_generic(const int64_t *mapping, int64_t nm, const int64_t *req, int
   scan_small(bcnt, nblk, boff, st);
   hipLaunchKernelGGL(k_scatter, dim3((unsigned)nblk), dim3(kThreads), 0, st, mapping, nmc,
                      (const int64_t *)nullptr, (const int64_t *)nullptr, (int64_t)0, t, t.slot_of,
-                     boff, nblk, unique, d_nunique);
+                     boff, nblk, unique, d_nunique, HostSizes{});
   DGS_LAUNCH_CHECK();
   if (nr > 0) {
     hipLaunchKernelGGL(k_relabel_req, dim3((unsigned)ceil_div(nr, kThreads)), dim3(kThreads), 0,

@@ -156,6 +156,7 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
 }
 
 Sampler::~Sampler() {
+  if (seq_ > 0) (void)hipStreamSynchronize(last_stream_);  // last relabel pass may still run
   delete indptr_srv_;
   delete indices_srv_;
   delete probs_srv_;
@@ -186,9 +187,19 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
                      int64_t *const *cols, int64_t *sizes, hipStream_t st) {
   if (L <= 0) return;
   sizes_.ensure(sizeof(int64_t) * (size_t)(3 * L + 1));
-  sizes_host_.ensure(sizeof(int64_t) * (size_t)(3 * L + 1));
+  if (sizes_host_.bytes < sizeof(int64_t) * (size_t)(3 * L + 2)) {
+    sizes_host_.flags = hipHostMallocCoherent | hipHostMallocMapped;
+    sizes_host_.ensure(sizeof(int64_t) * (size_t)(3 * L + 2));
+    sizes_host_.as<int64_t>()[0] = 0;
+    DGS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&sizes_host_dev_), sizes_host_.p, 0));
+  }
   int64_t *dsz = sizes_.as<int64_t>();
   int64_t *hsz = sizes_host_.as<int64_t>();
+  // The previous call may still be relabelling on its stream (see the wait below): a call on
+  // another stream first drains it, since both use this sampler's scratch.
+  if (seq_ > 0 && st != last_stream_) DGS_HIP(hipStreamSynchronize(last_stream_));
+  last_stream_ = st;
+  const uint64_t seq = ++seq_;
   std::vector<int64_t> fcap(L), ecap(L);
   bounds(n_seeds, fan_out, L, fcap.data(), ecap.data());
   const int64_t *cur = seeds;
@@ -205,20 +216,36 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
     ws_.table_dirty = true;
     // rows[h] receives each edge's seed row r from the sampler and is relabelled in place
     sample_hop(src_, cur, S, k, replace, bias_, seed, rows[h], cols[h], d_nnz, t, ws_, st);
+    // the last hop's scatter publishes every size to pinned host memory (no copy, no sync)
+    const HostSizes pub = h == L - 1 ? HostSizes{dsz, 3 * L, sizes_host_dev_, seq} : HostSizes{};
     relabel_hop(cur, S, cols[h], d_nnz, nnz_cap, /*seeds_unique=*/h > 0, t, frontiers[h],
-                rows[h], cols[h], d_uniq, ws_, st);
+                rows[h], cols[h], d_uniq, ws_, st, pub);
     cur = frontiers[h];
     S = Count{fcap[h], d_uniq};
   }
   profile_end(st, 1);
-  DGS_HIP(hipMemcpyAsync(hsz, dsz, sizeof(int64_t) * (size_t)(3 * L), hipMemcpyDeviceToHost, st));
-  DGS_HIP(hipStreamSynchronize(st));
+  // Wait for the published sizes only: the host returns while the last relabel pass still runs
+  // (every consumer of the outputs is ordered after it on the stream).  A failed kernel shows
+  // up through hipStreamQuery.
+  for (uint64_t spin = 1;; ++spin) {
+    if (__atomic_load_n(hsz, __ATOMIC_ACQUIRE) == (int64_t)seq) break;
+    if ((spin & 255) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) {
+        DGS_CHECK(__atomic_load_n(hsz, __ATOMIC_ACQUIRE) == (int64_t)seq,
+                  "sample: sizes were not published");
+        break;
+      }
+      if (q != hipErrorNotReady) DGS_HIP(q);
+    }
+    __builtin_ia32_pause();
+  }
   int64_t s = n_seeds;
   for (int h = 0; h < L; ++h) {
     sizes[3 * h + 0] = s;
-    sizes[3 * h + 1] = hsz[3 * h + 1];
-    sizes[3 * h + 2] = hsz[3 * h + 2];
-    s = hsz[3 * h + 1];
+    sizes[3 * h + 1] = hsz[1 + 3 * h + 1];
+    sizes[3 * h + 2] = hsz[1 + 3 * h + 2];
+    s = sizes[3 * h + 1];
   }
 }
 

@@ -83,7 +83,10 @@ class Sampler {
   RowSrc src_{};
   HopScratch ws_;
   DevBuf sizes_;
-  HostPinned sizes_host_;
+  HostPinned sizes_host_;  // [0] = publication sequence, [1..] = per-hop sizes
+  int64_t *sizes_host_dev_ = nullptr;
+  uint64_t seq_ = 0;
+  hipStream_t last_stream_ = nullptr;
 };
 
 class FeatureServer {

@@ -86,7 +86,19 @@ def check(rc):
         raise RuntimeError("dgs: " + lib.dgs_last_error().decode(errors="replace"))
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device=None):
+    """Current HIP stream of `device` (torch.device, index or None = current device)."""
+    if _raw_stream is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        elif isinstance(device, int):
+            idx = device
+        else:
+            idx = device.index if device.index is not None else torch.cuda.current_device()
+        return c_vp(_raw_stream(idx))
     return c_vp(torch.cuda.current_stream(device).cuda_stream)
 
 

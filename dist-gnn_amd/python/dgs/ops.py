@@ -262,8 +262,13 @@ def _CAPI_compute_frontier_heat_with_bias(seeds, indptr, indices, probs, seeds_h
     return _heat(seeds, indptr, indices, probs, seeds_heat, num_picks, indptr_diff)
 
 
+PROFILE_GATHER, PROFILE_SAMPLE, PROFILE_SELECT = 1, 2, 4
+
+
 def profile_enable(on=True):
-    check(lib.dgs_profile_enable(int(bool(on))))
+    """ADDITIVE instrumentation: True = everything, False = off, or a PROFILE_* bit mask."""
+    mask = (7 if on else 0) if isinstance(on, bool) else int(on)
+    check(lib.dgs_profile_enable(mask))
 
 
 def profile_read():

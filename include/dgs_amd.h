@@ -178,12 +178,18 @@ int dgs_feature_server_layout(const dgs_feature_server *s, int *wshift);
 int dgs_feature_server_destroy(dgs_feature_server *s);
 
 /* ------------------------------------------------------------------------------------
- * Instrumentation (bench.py).  When enabled, gather kernels are launched with
- * hipExtLaunchKernelGGL start/stop events (recorded by the GPU at the kernel's own start and
- * end, on the stream it runs on) and every sampling hop is bracketed by stream events.
- * dgs_profile_read() returns the summed milliseconds and counts, then resets them.
+ * Instrumentation (bench.py).  `mask` selects what is timed: DGS_PROFILE_GATHER = feature-
+ * server gather kernels, DGS_PROFILE_SELECT = index_select kernels (both launched with
+ * hipExtLaunchKernelGGL start/stop events, recorded by the GPU at the kernel's own start and
+ * end on the stream it runs on), DGS_PROFILE_SAMPLE = whole sample calls (one stream event
+ * before the first and one after the last kernel).  0 disables; any nonzero value outside the
+ * three bits enables all.  dgs_profile_read() returns the summed milliseconds and counts, then
+ * resets them.
  * ---------------------------------------------------------------------------------- */
-int dgs_profile_enable(int on);
+#define DGS_PROFILE_GATHER 1
+#define DGS_PROFILE_SAMPLE 2
+#define DGS_PROFILE_SELECT 4
+int dgs_profile_enable(int mask);
 int dgs_profile_read(double *gather_ms, int64_t *gather_launches, double *sample_ms,
                      int64_t *sample_calls, double *select_ms, int64_t *select_launches);
 
