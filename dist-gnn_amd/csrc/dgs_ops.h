@@ -73,6 +73,7 @@ struct HopScratch {
       misc, cdf;
   HostPinned host;
   uint64_t table_cap = 0;  // capacity currently allocated and clean
+  uint64_t hop_serial = 0;  // parity selects the hub counter of a hop
   bool table_dirty = false;
 };
 
@@ -88,6 +89,10 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count S, int64_t k, boo
 // Clean relabel table with capacity for n_ub insertions (marks the scratch dirty until the
 // hop's relabel pass has returned the touched slots to empty).
 Table relabel_table(HopScratch &ws, int64_t n_ub, hipStream_t st);
+// Direct-layout table over node ids [0, num_nodes) (val = empty everywhere on return; a table
+// left dirty by an interrupted hop is re-filled).  The relabel pass of every hop empties the
+// entries it touched, so a completed hop leaves it clean.
+Table direct_table(DevBuf &val, DevBuf &lab, int64_t num_nodes, bool *dirty, hipStream_t st);
 
 // Relabel for the node-classification hop: mapping = cat(seeds[S], col[nnz]) where nnz is
 // read from d_nnz (device); writes unique ids to `unique` (first-occurrence order),

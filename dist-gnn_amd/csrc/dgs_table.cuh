@@ -10,12 +10,17 @@ namespace dgs {
 constexpr int64_t kTableEmpty = -1;
 constexpr int32_t kTableNoPos = 0x7FFFFFFF;
 
+// Two layouts.  Hashed (key != nullptr): open addressing over arbitrary int64 ids (the
+// standalone relabel op).  Direct (direct == true): the sampler's ids are graph node ids in
+// [0, N), so val / lab are indexed by the id itself -- one load and at most one atomicMin per
+// insert, no probing, no key CAS and no slot_of bookkeeping (2 x 4 bytes of HBM per node).
 struct Table {
-  int64_t *key;   // nullptr: no table (standalone sampling op)
-  int32_t *val;   // minimum position (first occurrence)
-  int32_t *lab;   // label = rank among first occurrences
-  uint32_t *slot_of;  // slot of every inserted position
+  int64_t *key;   // hashed layout: slot keys; nullptr with !direct: no table (standalone op)
+  int32_t *val;   // minimum position (first occurrence), per slot or per node
+  int32_t *lab;   // label = rank among first occurrences, per slot or per node
+  uint32_t *slot_of;  // hashed layout: slot of every inserted position
   uint64_t mask;
+  bool direct;
 };
 
 #ifdef __HIPCC__
@@ -49,7 +54,12 @@ __device__ __forceinline__ uint32_t table_insert(const Table &t, int64_t x, int3
 }
 
 __device__ __forceinline__ void table_record(const Table &t, int64_t x, int64_t pos) {
-  if (t.key) t.slot_of[pos] = table_insert(t, x, (int32_t)pos);
+  if (t.direct) {
+    // val only decreases: skip the atomic when an earlier occurrence is already recorded
+    if (t.val[x] > (int32_t)pos) atomicMin(t.val + x, (int32_t)pos);
+  } else if (t.key) {
+    t.slot_of[pos] = table_insert(t, x, (int32_t)pos);
+  }
 }
 
 __device__ __forceinline__ int64_t table_find(const Table &t, int64_t x) {

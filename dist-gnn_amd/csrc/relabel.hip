@@ -111,6 +111,75 @@ __global__ __launch_bounds__(kThreads) void k_relabel_hop(Count nac, const int64
   }
 }
 
+// ---- direct layout (sampler hops): val / lab indexed by node id, element i of cat(seeds, col)
+__global__ __launch_bounds__(kThreads) void k_dflag_count(const int64_t *a, Count nac,
+                                                          const int64_t *b, const int64_t *d_nb,
+                                                          Table t, int64_t *bcnt) {
+  __shared__ int64_t lds[kThreads / 64];
+  const int64_t na = nac.get();
+  const int64_t n = na + *d_nb;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int64_t f = (i < n && t.val[elem(a, na, b, i)] == (int32_t)i) ? 1 : 0;
+  const int64_t s = block_sum<kThreads>(f, lds);
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kThreads) void k_dscatter(const int64_t *a, Count nac,
+                                                       const int64_t *b, const int64_t *d_nb,
+                                                       Table t, const int64_t *boff,
+                                                       int64_t nblocks, int64_t *unique,
+                                                       int64_t *d_nunique, HostSizes pub) {
+  __shared__ int64_t lds[kThreads / 64];
+  const int64_t na = nac.get();
+  const int64_t n = na + *d_nb;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  int64_t x = 0, f = 0;
+  if (i < n) {
+    x = elem(a, na, b, i);
+    f = t.val[x] == (int32_t)i ? 1 : 0;
+  }
+  int64_t tot;
+  const int64_t ex = block_exclusive_scan<kThreads>(f, &tot, lds);
+  if (f) {
+    const int64_t pos = boff[blockIdx.x] + ex;
+    unique[pos] = x;
+    t.lab[x] = (int32_t)pos;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *d_nunique = boff[nblocks];
+    if (pub.host) {
+      for (int64_t j = 0; j < pub.n; ++j)
+        __hip_atomic_store(pub.host + 1 + j, pub.dev[j], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(pub.host, (int64_t)pub.seq, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// out_col[e] = lab[col[e]] in place; out_row[e] = lab[seeds[r]] when the seeds may repeat
+// (else label(r) == r, see k_relabel_hop); then every touched node's val returns to empty.
+__global__ __launch_bounds__(kThreads) void k_drelabel_hop(const int64_t *seeds, Count nac,
+                                                           const int64_t *d_nb, Table t,
+                                                           int remap_rows, int64_t *out_row,
+                                                           int64_t *out_col) {
+  const int64_t na = nac.get();
+  const int64_t nb = *d_nb;
+  const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (e < nb) {
+    const int64_t v = out_col[e];
+    out_col[e] = t.lab[v];
+    if (remap_rows) out_row[e] = t.lab[seeds[out_row[e]]];
+    t.val[v] = kNoPos;
+  }
+  if (e < na) t.val[seeds[e]] = kNoPos;
+}
+
+__global__ void k_fill_i32(int32_t *p, int64_t n, int32_t v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
 // Generic relabel: req lookups (absent -> -1, tensor_relabel.cu:47-61).
 __global__ __launch_bounds__(kThreads) void k_relabel_req(Table t, const int64_t *req,
                                                           int64_t nr, int64_t *out) {
@@ -157,7 +226,20 @@ Table relabel_table(HopScratch &ws, int64_t n_ub, hipStream_t st) {
   }
   ws.slot_of.ensure(sizeof(uint32_t) * (size_t)(n_ub > 0 ? n_ub : 1));
   return Table{ws.tkey.as<int64_t>(), ws.tval.as<int32_t>(), ws.tlab.as<int32_t>(),
-               ws.slot_of.as<uint32_t>(), cap - 1};
+               ws.slot_of.as<uint32_t>(), cap - 1, false};
+}
+
+Table direct_table(DevBuf &val, DevBuf &lab, int64_t num_nodes, bool *dirty, hipStream_t st) {
+  const int64_t n = num_nodes > 0 ? num_nodes : 1;
+  const bool fresh = val.ensure(sizeof(int32_t) * (size_t)n);
+  lab.ensure(sizeof(int32_t) * (size_t)n);
+  if (fresh || *dirty) {
+    hipLaunchKernelGGL(k_fill_i32, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st,
+                       val.as<int32_t>(), n, kNoPos);
+    DGS_LAUNCH_CHECK();
+    *dirty = false;
+  }
+  return Table{nullptr, val.as<int32_t>(), lab.as<int32_t>(), nullptr, 0, true};
 }
 
 // The hop's seeds and sampled neighbours were already inserted by the sampling kernels
@@ -172,6 +254,19 @@ void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64
   ws.misc.ensure(sizeof(int64_t) * (size_t)(2 * nblk + 2));
   int64_t *bcnt = ws.misc.as<int64_t>();
   int64_t *boff = bcnt + nblk;
+  if (t.direct) {
+    hipLaunchKernelGGL(k_dflag_count, dim3((unsigned)nblk), dim3(kThreads), 0, st, seeds, Sc,
+                       col, d_nnz, t, bcnt);
+    DGS_LAUNCH_CHECK();
+    scan_small(bcnt, nblk, boff, st);
+    hipLaunchKernelGGL(k_dscatter, dim3((unsigned)nblk), dim3(kThreads), 0, st, seeds, Sc, col,
+                       d_nnz, t, boff, nblk, unique, d_nunique, pub);
+    DGS_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_drelabel_hop, dim3((unsigned)nblk), dim3(kThreads), 0, st, seeds, Sc,
+                       d_nnz, t, (int)!seeds_unique, out_row, out_col);
+    DGS_LAUNCH_CHECK();
+    return;
+  }
   hipLaunchKernelGGL(k_flag_count, dim3((unsigned)nblk), dim3(kThreads), 0, st, Sc, d_nnz,
                      (int64_t)0, t, t.slot_of, bcnt);
   DGS_LAUNCH_CHECK();

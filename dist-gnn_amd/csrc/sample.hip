@@ -98,9 +98,12 @@ __global__ __launch_bounds__(kTileRows) void k_prep(RowSrc src, const int64_t *_
                                                     int32_t *__restrict__ tpre2,
                                                     int64_t *__restrict__ bsum,
                                                     int64_t *__restrict__ tsum, HubView hub,
-                                                    int32_t *__restrict__ hubslot, Table table) {
+                                                    int32_t *__restrict__ hubslot, Table table,
+                                                    int64_t *next_hub_count) {
   __shared__ int64_t lds[kTileRows / 64];
   const int64_t S = Sc.get();
+  // the next hop's counter was last used two hops ago: reset it here (no memset launch)
+  if (blockIdx.x == 0 && threadIdx.x == 0) *next_hub_count = 0;
   if ((int64_t)blockIdx.x * kTileRows >= S) return;  // whole workgroup past the live rows
   const int64_t i = (int64_t)blockIdx.x * kTileRows + threadIdx.x;
   int64_t cnt = 0, tdeg = 0;
@@ -172,22 +175,49 @@ __device__ __forceinline__ uint32_t mod_big(uint32_t x, uint32_t d) {
 }
 
 // ------------------------------------------------------------------------------------
-// Hub reservoir: every wave takes 512-edge chunks (idx = k + 512q + t + 128w, t < 128,
-// w < 4 <-> one Philox block per logical thread t) of any hub row and folds its picks into
-// the row's k slots with atomicMax (rowwise_sampling.cu:85-92).
-__global__ __launch_bounds__(256) void k_hub_reservoir(const RowInfo *__restrict__ rowinfo,
-                                                       Count Sc, int64_t k, uint64_t seed,
-                                                       HubView hub, int32_t *hubslot) {
-  const int64_t S = Sc.get();
+// Uniform sampling (rowwise_sampling.cu K2/K3).  Arguments shared by the kernels below.
+struct UniformArgs {
+  RowSrc src;
+  Count Sc;
+  int64_t k;
+  uint64_t seed;
+  const RowInfo *rowinfo;
+  const int32_t *tpre;
+  const int64_t *boff;
+  HubView hub;
+  int32_t *hubslot;
+  int64_t *rowpos;
+  int64_t *col;
+  Table table;
+};
+
+// Writes the k picks of row r whose reservoir slots are `slots` (16-lane group, lane L).
+__device__ __forceinline__ void emit_slots(const UniformArgs &a, int64_t S, int64_t r,
+                                           const int64_t *nb, int64_t out,
+                                           const int32_t *slots, int L) {
+  for (int64_t s2 = L; s2 < a.k; s2 += kGroup) {
+    const int64_t v = nb[slots[s2]];
+    a.rowpos[out + s2] = r;
+    a.col[out + s2] = v;
+    table_record(a.table, v, S + out + s2);
+  }
+}
+
+// Hub reservoir: wave gw of nwaves takes a contiguous range of 512-edge chunks
+// (idx = k + 512q + t + 128w, t < 128, w < 4 <-> one Philox block per logical thread t) of the
+// hub rows and folds their picks into the rows' k global slots with atomicMax
+// (rowwise_sampling.cu:85-92; any split gives the same maxima).
+__device__ __forceinline__ void hub_reservoir(const UniformArgs &a, int64_t gw, int64_t nwaves) {
+  const int64_t S = a.Sc.get();
+  const int64_t k = a.k;
+  const HubView &hub = a.hub;
   const uint64_t packed = (uint64_t)*hub.count;
   const int64_t H = (int64_t)(packed >> kHubShift);
   if (H == 0) return;
   const int64_t total = (int64_t)(packed & kHubChunkMask);
   const int lane = threadIdx.x & 63;
-  // Each wave owns one contiguous range of chunks: one binary search per wave, then the hub
-  // index only moves forward (a dependent search per chunk would dominate the Philox work).
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  // One binary search per wave, then the hub index only moves forward (a dependent search per
+  // chunk would dominate the Philox work).
   const int64_t c0 = total * gw / nwaves, c1 = total * (gw + 1) / nwaves;
   if (c0 >= c1) return;
   int64_t lo = 0, hi = H;  // largest h with cptr[h] <= c0
@@ -198,19 +228,19 @@ __global__ __launch_bounds__(256) void k_hub_reservoir(const RowInfo *__restrict
   int64_t h = lo;
   int64_t hstart = hub.cptr[h], hnext = h + 1 < H ? hub.cptr[h + 1] : total;
   int64_t r = hub.row[h];
-  int64_t deg = ri_deg(rowinfo[r]);
+  int64_t deg = ri_deg(a.rowinfo[r]);
   for (int64_t c = c0; c < c1; ++c) {
     while (c >= hnext) {
       ++h;
       hstart = hnext;
       hnext = h + 1 < H ? hub.cptr[h + 1] : total;
       r = hub.row[h];
-      deg = ri_deg(rowinfo[r]);
+      deg = ri_deg(a.rowinfo[r]);
     }
     const int64_t q = c - hstart;
-    const uint64_t key = wave_uniform(seed * (uint64_t)S + (uint64_t)r);
+    const uint64_t key = wave_uniform(a.seed * (uint64_t)S + (uint64_t)r);
     const uint2 kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
-    int32_t *sl = hubslot + h * k;
+    int32_t *sl = a.hubslot + h * k;
     const uint4 o4a = philox4x32_10(
         make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)lane, 0u), kk);
     const uint4 o4b = philox4x32_10(
@@ -248,29 +278,22 @@ __global__ __launch_bounds__(256) void k_hub_reservoir(const RowInfo *__restrict
   }
 }
 
-// ------------------------------------------------------------------------------------
-// Uniform sampling of one 256-row tile.  16-lane groups own rows.
+// Rows of one 16-row block, a 16-lane group per row.  A hub row (hubid >= 0) takes its k picks
+// from the global slots k_hub_reservoir filled.
 template <bool kReplace>
-__global__ __launch_bounds__(kTileRows) void k_sample_uniform(
-    RowSrc src, Count Sc, int64_t k, uint64_t seed, const RowInfo *__restrict__ rowinfo,
-    const int32_t *__restrict__ tpre, const int64_t *__restrict__ boff, HubView hub,
-    const int32_t *__restrict__ hubslot, int use_hubs, int64_t *__restrict__ rowpos,
-    int64_t *__restrict__ col, Table table) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  int32_t *s_slot = reinterpret_cast<int32_t *>(smem);  // [16 groups][k]
-  const int64_t S = Sc.get();
-  // the hub counter is consumed by now (k_hub_reservoir ran before this kernel): reset it for
-  // the next hop instead of a separate memset
-  if (use_hubs && blockIdx.x == 0 && threadIdx.x == 0) *hub.count = 0;
+__device__ __forceinline__ void sample_rows(const UniformArgs &a, int64_t blk, int32_t *s_slot,
+                                            bool use_hubs) {
+  const int64_t S = a.Sc.get();
+  const int64_t k = a.k;
   const int g = threadIdx.x / kGroup, L = threadIdx.x % kGroup;
-  const int64_t r = (int64_t)blockIdx.x * kRowsPerBlock + g;
+  const int64_t r = blk * kRowsPerBlock + g;
   if (r >= S) return;
   int32_t *sl = s_slot + g * k;
-  const RowInfo ri = rowinfo[r];
+  const RowInfo ri = a.rowinfo[r];
   const int64_t deg = ri_deg(ri);
   const int64_t *nb = ri.ptr;
-  const int64_t out = boff[r / kTileRows] + tpre[r];
-  const uint64_t key = seed * (uint64_t)S + (uint64_t)r;
+  const int64_t out = a.boff[r / kTileRows] + a.tpre[r];
+  const uint64_t key = a.seed * (uint64_t)S + (uint64_t)r;
   const uint2 kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
   if (kReplace) {
     if (deg > 0) {
@@ -280,9 +303,9 @@ __global__ __launch_bounds__(kTileRows) void k_sample_uniform(
         const uint32_t x = u4_get(o4, (int)(j & 3));
         const int64_t e = (int64_t)x % deg;
         const int64_t v = nb[e];
-        rowpos[out + p] = r;
-        col[out + p] = v;
-        table_record(table, v, S + out + p);
+        a.rowpos[out + p] = r;
+        a.col[out + p] = v;
+        table_record(a.table, v, S + out + p);
       }
     }
     return;
@@ -290,46 +313,51 @@ __global__ __launch_bounds__(kTileRows) void k_sample_uniform(
   if (deg <= k) {
     for (int64_t p = L; p < deg; p += kGroup) {
       const int64_t v = nb[p];
-      rowpos[out + p] = r;
-      col[out + p] = v;
-      table_record(table, v, S + out + p);
+      a.rowpos[out + p] = r;
+      a.col[out + p] = v;
+      table_record(a.table, v, S + out + p);
     }
     return;
   }
-  const int64_t h = use_hubs ? hub.hubid[r] : -1;
-  const int32_t *slots = sl;
+  const int64_t h = use_hubs ? a.hub.hubid[r] : -1;
   if (h >= 0) {
-    slots = hubslot + h * k;
-  } else {
-    for (int64_t s2 = L; s2 < k; s2 += kGroup) sl[s2] = (int32_t)s2;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    for (int64_t q = 0; k + 512 * q < deg; ++q) {
-      for (int tt = 0; tt < 128 / kGroup; ++tt) {
-        const int t = L + kGroup * tt;
-        const int64_t base = k + t + 512 * q;
-        if (base >= deg) break;
-        const uint4 o4 = philox4x32_10(
-            make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)t, 0u), kk);
+    emit_slots(a, S, r, nb, out, a.hubslot + h * k, L);
+    return;
+  }
+  for (int64_t s2 = L; s2 < k; s2 += kGroup) sl[s2] = (int32_t)s2;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  for (int64_t q = 0; k + 512 * q < deg; ++q) {
+    for (int tt = 0; tt < 128 / kGroup; ++tt) {
+      const int t = L + kGroup * tt;
+      const int64_t base = k + t + 512 * q;
+      if (base >= deg) break;
+      const uint4 o4 = philox4x32_10(
+          make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)t, 0u), kk);
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const int64_t idx = base + 128 * w;
-          if (idx < deg) {
-            const uint32_t num = u4_get(o4, w) % (uint32_t)(idx + 1);
-            if ((int64_t)num < k) atomicMax(sl + num, (int32_t)idx);
-          }
+      for (int w = 0; w < 4; ++w) {
+        const int64_t idx = base + 128 * w;
+        if (idx < deg) {
+          const uint32_t num = u4_get(o4, w) % (uint32_t)(idx + 1);
+          if ((int64_t)num < k) atomicMax(sl + num, (int32_t)idx);
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
   }
-  for (int64_t s2 = L; s2 < k; s2 += kGroup) {
-    const int64_t v = nb[slots[s2]];
-    rowpos[out + s2] = r;
-    col[out + s2] = v;
-    table_record(table, v, S + out + s2);
-  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  emit_slots(a, S, r, nb, out, sl, L);
+}
+
+__global__ __launch_bounds__(256) void k_hub_reservoir(UniformArgs a) {
+  hub_reservoir(a, ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6,
+                ((int64_t)gridDim.x * blockDim.x) >> 6);
+}
+
+template <bool kReplace>
+__global__ __launch_bounds__(kTileRows) void k_sample_uniform(UniformArgs a, int use_hubs) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  sample_rows<kReplace>(a, blockIdx.x, reinterpret_cast<int32_t *>(smem), use_hubs != 0);
 }
 
 // ------------------------------------------------------------------------------------
@@ -556,12 +584,14 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     return;
   }
   const bool use_hubs = !bias && !replace && k > 0 && S < kHubMaxRows;
-  // the hub counter lives in its own buffer: zeroed at allocation, then reset on the device by
-  // every hop that used it
-  if (ws.hubcount.ensure(64)) DGS_HIP(hipMemsetAsync(ws.hubcount.p, 0, 64, st));
+  // Two hub counters used by alternate hops (a global hop serial, so calls chain correctly):
+  // each prep zeroes the other one; zeroed once at allocation.
+  if (ws.hubcount.ensure(128)) DGS_HIP(hipMemsetAsync(ws.hubcount.p, 0, 128, st));
+  const uint64_t par = ws.hop_serial++ & 1;
   ws.hub.ensure(HubView::bytes(S));
   HubView hub = HubView::make(ws.hub.as<int64_t>(), S);
-  hub.count = ws.hubcount.as<int64_t>();
+  hub.count = ws.hubcount.as<int64_t>() + 8 * par;
+  int64_t *next_count = ws.hubcount.as<int64_t>() + 8 * (par ^ 1);
   const bool bias_replace = bias && replace;
   ws.tpre.ensure(sizeof(int32_t) * (size_t)(2 * S));
   int32_t *tpre = ws.tpre.as<int32_t>();
@@ -569,7 +599,7 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   if (use_hubs) ws.hubslot.ensure(sizeof(int32_t) * (size_t)(S * k));
   hipLaunchKernelGGL(k_prep, dim3((unsigned)nb), dim3(kTileRows), 0, st, src, seeds, Sc, k,
                      (int)replace, (int)use_hubs, (int)bias_replace, rowinfo, tpre, tpre2, bsum,
-                     tsum, hub, ws.hubslot.as<int32_t>(), table);
+                     tsum, hub, ws.hubslot.as<int32_t>(), table, next_count);
   DGS_LAUNCH_CHECK();
   if (k == 0) {  // seeds still enter the relabel table (frontier = unique(seeds))
     DGS_HIP(hipMemsetAsync(d_nnz, 0, sizeof(int64_t), st));
@@ -581,22 +611,21 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   DGS_LAUNCH_CHECK();
 
   if (!bias) {
+    DGS_CHECK(replace || k <= kMaxPicksLds, "num_picks > 512 is not supported without replacement");
+    const UniformArgs ua{src, Sc, k, launch_seed, rowinfo, tpre, boff, hub,
+                         ws.hubslot.as<int32_t>(), rowpos, col, table};
+    const size_t lds = replace ? 16 : sizeof(int32_t) * (size_t)kRowsPerBlock * k;
+    const int64_t row_blocks = ceil_div(S, kRowsPerBlock);
     if (use_hubs) {
-      hipLaunchKernelGGL(k_hub_reservoir, dim3(kHubBlocks), dim3(256), 0, st, rowinfo, Sc, k,
-                         launch_seed, hub, ws.hubslot.as<int32_t>());
+      hipLaunchKernelGGL(k_hub_reservoir, dim3(kHubBlocks), dim3(256), 0, st, ua);
       DGS_LAUNCH_CHECK();
     }
-    DGS_CHECK(replace || k <= kMaxPicksLds, "num_picks > 512 is not supported without replacement");
-    const size_t lds = replace ? 16 : sizeof(int32_t) * (size_t)kRowsPerBlock * k;
-    const dim3 grid((unsigned)ceil_div(S, kRowsPerBlock));
     if (replace)
-      hipLaunchKernelGGL(k_sample_uniform<true>, grid, dim3(kTileRows), lds, st, src, Sc, k,
-                         launch_seed, rowinfo, tpre, boff, hub, ws.hubslot.as<int32_t>(), 0,
-                         rowpos, col, table);
+      hipLaunchKernelGGL(k_sample_uniform<true>, dim3((unsigned)row_blocks), dim3(kTileRows),
+                         lds, st, ua, 0);
     else
-      hipLaunchKernelGGL(k_sample_uniform<false>, grid, dim3(kTileRows), lds, st, src, Sc, k,
-                         launch_seed, rowinfo, tpre, boff, hub, ws.hubslot.as<int32_t>(), 1,
-                         rowpos, col, table);
+      hipLaunchKernelGGL(k_sample_uniform<false>, dim3((unsigned)row_blocks), dim3(kTileRows),
+                         lds, st, ua, (int)use_hubs);
     DGS_LAUNCH_CHECK();
   } else {
     DGS_CHECK(k <= 32, "biased sampling supports num_picks <= 32 (rowwise_sampling_bias.cu:73)");

@@ -212,14 +212,15 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
     const int64_t nnz_cap = ecap[h];
     int64_t *d_nnz = dsz + 3 * h + 2;
     int64_t *d_uniq = dsz + 3 * h + 1;
-    const Table t = relabel_table(ws_, S.v + nnz_cap, st);
-    ws_.table_dirty = true;
+    const Table t = direct_table(dval_, dlab_, num_nodes_, &dtab_dirty_, st);
+    dtab_dirty_ = true;
     // rows[h] receives each edge's seed row r from the sampler and is relabelled in place
     sample_hop(src_, cur, S, k, replace, bias_, seed, rows[h], cols[h], d_nnz, t, ws_, st);
     // the last hop's scatter publishes every size to pinned host memory (no copy, no sync)
     const HostSizes pub = h == L - 1 ? HostSizes{dsz, 3 * L, sizes_host_dev_, seq} : HostSizes{};
     relabel_hop(cur, S, cols[h], d_nnz, nnz_cap, /*seeds_unique=*/h > 0, t, frontiers[h],
                 rows[h], cols[h], d_uniq, ws_, st, pub);
+    dtab_dirty_ = false;  // the relabel pass just enqueued empties what this hop touched
     cur = frontiers[h];
     S = Count{fcap[h], d_uniq};
   }
