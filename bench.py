@@ -37,8 +37,8 @@ def log(*a):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch", type=int, default=1024)
     p.add_argument("--fan-out", type=str, default="15,10,5")
     p.add_argument("--scale", type=int, default=21)   # products-like: 2,097,152 nodes

@@ -111,49 +111,92 @@ __global__ __launch_bounds__(kThreads) void k_relabel_hop(Count nac, const int64
   }
 }
 
-// ---- direct layout (sampler hops): val / lab indexed by node id, element i of cat(seeds, col)
-__global__ __launch_bounds__(kThreads) void k_dflag_count(const int64_t *a, Count nac,
-                                                          const int64_t *b, const int64_t *d_nb,
-                                                          Table t, int64_t *bcnt) {
+// ---- direct layout (sampler hops): val / lab indexed by node id
+// First occurrences, two passes over 1024-element tiles (4 contiguous elements per thread):
+// element i of cat(seeds, col) is a first occurrence iff val[x] == i, and its label is its rank
+// among first occurrences.  Pass 1 counts per tile; pass 2 sums the counts of all earlier tiles
+// directly (a few hundred L2-resident words) instead of a separate scan launch, then scatters.
+constexpr int kCompactItems = 4;
+constexpr int64_t kCompactTile = (int64_t)kThreads * kCompactItems;
+
+__device__ __forceinline__ void publish_sizes(const HostSizes &pub) {
+  if (!pub.host) return;
+  for (int64_t j = 0; j < pub.n; ++j)
+    __hip_atomic_store(pub.host + 1 + j, pub.dev[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(pub.host, (int64_t)pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Branch-free flags of this thread's elements: out-of-range ones are clamped to the last
+// element and dropped, so all id loads issue back to back, then all val loads.
+__device__ __forceinline__ int64_t first_flags(const int64_t *a, int64_t na, const int64_t *b,
+                                               int64_t n, const Table &t, int64_t i0,
+                                               int64_t (&x)[kCompactItems],
+                                               bool (&f)[kCompactItems]) {
+  int32_t pv[kCompactItems];
+#pragma unroll
+  for (int j = 0; j < kCompactItems; ++j) {
+    const int64_t i = i0 + j < n ? i0 + j : n - 1;
+    const int64_t *src = i < na ? a + i : b + (i - na);
+    x[j] = *src;
+  }
+#pragma unroll
+  for (int j = 0; j < kCompactItems; ++j) pv[j] = t.val[x[j]];
+  int64_t cnt = 0;
+#pragma unroll
+  for (int j = 0; j < kCompactItems; ++j) {
+    f[j] = i0 + j < n && pv[j] == (int32_t)(i0 + j);
+    cnt += f[j];
+  }
+  return cnt;
+}
+
+__global__ __launch_bounds__(kThreads) void k_dcount(const int64_t *a, Count nac,
+                                                     const int64_t *b, const int64_t *d_nb,
+                                                     Table t, int64_t *tcnt) {
   __shared__ int64_t lds[kThreads / 64];
   const int64_t na = nac.get();
   const int64_t n = na + *d_nb;
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int64_t f = (i < n && t.val[elem(a, na, b, i)] == (int32_t)i) ? 1 : 0;
-  const int64_t s = block_sum<kThreads>(f, lds);
-  if (threadIdx.x == 0) bcnt[blockIdx.x] = s;
+  const int64_t i0 = (int64_t)blockIdx.x * kCompactTile + (int64_t)threadIdx.x * kCompactItems;
+  if ((int64_t)blockIdx.x * kCompactTile >= n) return;
+  int64_t x[kCompactItems];
+  bool f[kCompactItems];
+  const int64_t cnt = first_flags(a, na, b, n, t, i0, x, f);
+  const int64_t s = block_sum<kThreads>(cnt, lds);
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = s;
 }
 
 __global__ __launch_bounds__(kThreads) void k_dscatter(const int64_t *a, Count nac,
                                                        const int64_t *b, const int64_t *d_nb,
-                                                       Table t, const int64_t *boff,
-                                                       int64_t nblocks, int64_t *unique,
-                                                       int64_t *d_nunique, HostSizes pub) {
+                                                       Table t, const int64_t *tcnt,
+                                                       int64_t *unique, int64_t *d_nunique,
+                                                       HostSizes pub) {
   __shared__ int64_t lds[kThreads / 64];
   const int64_t na = nac.get();
   const int64_t n = na + *d_nb;
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  int64_t x = 0, f = 0;
-  if (i < n) {
-    x = elem(a, na, b, i);
-    f = t.val[x] == (int32_t)i ? 1 : 0;
-  }
+  const int64_t tile = blockIdx.x;
+  const int64_t ntiles = (n + kCompactTile - 1) / kCompactTile;
+  if (tile >= ntiles) return;
+  // this tile's offset: sum of the earlier tiles' counts (issued before the element loads)
+  int64_t pre = 0;
+  for (int64_t j = threadIdx.x; j < tile; j += kThreads) pre += tcnt[j];
+  const int64_t i0 = tile * kCompactTile + (int64_t)threadIdx.x * kCompactItems;
+  int64_t x[kCompactItems];
+  bool f[kCompactItems];
+  const int64_t cnt = first_flags(a, na, b, n, t, i0, x, f);
+  const int64_t base = block_sum<kThreads>(pre, lds);
   int64_t tot;
-  const int64_t ex = block_exclusive_scan<kThreads>(f, &tot, lds);
-  if (f) {
-    const int64_t pos = boff[blockIdx.x] + ex;
-    unique[pos] = x;
-    t.lab[x] = (int32_t)pos;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *d_nunique = boff[nblocks];
-    if (pub.host) {
-      for (int64_t j = 0; j < pub.n; ++j)
-        __hip_atomic_store(pub.host + 1 + j, pub.dev[j], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(pub.host, (int64_t)pub.seq, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+  int64_t ex = base + block_exclusive_scan<kThreads>(cnt, &tot, lds);
+#pragma unroll
+  for (int j = 0; j < kCompactItems; ++j) {
+    if (f[j]) {
+      unique[ex] = x[j];
+      t.lab[x[j]] = (int32_t)ex;
+      ++ex;
     }
+  }
+  if (tile == ntiles - 1 && threadIdx.x == 0) {
+    *d_nunique = base + tot;
+    publish_sizes(pub);
   }
 }
 
@@ -255,12 +298,13 @@ void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64
   int64_t *bcnt = ws.misc.as<int64_t>();
   int64_t *boff = bcnt + nblk;
   if (t.direct) {
-    hipLaunchKernelGGL(k_dflag_count, dim3((unsigned)nblk), dim3(kThreads), 0, st, seeds, Sc,
-                       col, d_nnz, t, bcnt);
+    const int64_t ntiles = ceil_div(n_ub > 0 ? n_ub : 1, kCompactTile);
+    int64_t *tcnt = bcnt;  // ws.misc holds >= nblk >= ntiles words
+    hipLaunchKernelGGL(k_dcount, dim3((unsigned)ntiles), dim3(kThreads), 0, st, seeds, Sc, col,
+                       d_nnz, t, tcnt);
     DGS_LAUNCH_CHECK();
-    scan_small(bcnt, nblk, boff, st);
-    hipLaunchKernelGGL(k_dscatter, dim3((unsigned)nblk), dim3(kThreads), 0, st, seeds, Sc, col,
-                       d_nnz, t, boff, nblk, unique, d_nunique, pub);
+    hipLaunchKernelGGL(k_dscatter, dim3((unsigned)ntiles), dim3(kThreads), 0, st, seeds, Sc,
+                       col, d_nnz, t, (const int64_t *)tcnt, unique, d_nunique, pub);
     DGS_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_drelabel_hop, dim3((unsigned)nblk), dim3(kThreads), 0, st, seeds, Sc,
                        d_nnz, t, (int)!seeds_unique, out_row, out_col);

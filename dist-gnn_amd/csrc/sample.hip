@@ -27,7 +27,7 @@ namespace {
 constexpr int kTileRows = 256;   // rows per prep / sample workgroup
 constexpr int kGroup = 16;       // lanes per row in the uniform kernel
 constexpr int kRowsPerBlock = kTileRows / kGroup;  // rows per uniform-sampling workgroup
-constexpr int kHubT = 1024;      // reservoir tail length above which a row is split
+constexpr int kHubT = 128;       // reservoir tail length above which a row goes to the hub kernel
 constexpr int kHubBlocks = 2048; // workgroups of the hub kernel (8 waves per SIMD)
 constexpr int kMaxPicksLds = 512;
 constexpr int kScanThreads = 1024;

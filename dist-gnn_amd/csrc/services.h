@@ -85,7 +85,7 @@ class Sampler {
   DevBuf dval_, dlab_;  // direct relabel table over node ids (first position, label)
   bool dtab_dirty_ = false;
   DevBuf sizes_;
-  HostPinned sizes_host_;  // [0] = publication sequence, [1..] = per-hop sizes
+  HostPinned sizes_host_;  // [0] publication sequence, [1..3L] per-hop sizes
   int64_t *sizes_host_dev_ = nullptr;
   uint64_t seq_ = 0;
   hipStream_t last_stream_ = nullptr;
