@@ -349,7 +349,20 @@ __device__ __forceinline__ void sample_rows(const UniformArgs &a, int64_t blk, i
   emit_slots(a, S, r, nb, out, sl, L);
 }
 
-__global__ __launch_bounds__(256) void k_hub_reservoir(UniformArgs a) {
+// Hub kernel.  Its workgroup 0 first does the hop's tile-offset scan (k_scan_hop's job:
+// boff[0..nb] from the prep tile sums, nnz), which the sampling kernel after it reads -- one
+// launch fewer per hop.
+__global__ __launch_bounds__(256) void k_hub_reservoir(UniformArgs a, const int64_t *bsum,
+                                                       int64_t *boff, int64_t *d_nnz) {
+  if (blockIdx.x == 0) {
+    __shared__ int64_t lds[256 / 64];
+    const int64_t nb = (a.Sc.get() + kTileRows - 1) / kTileRows;
+    const int64_t tot = block_scan_range<256, 8>(bsum, nb, boff, lds);
+    if (threadIdx.x == 0) {
+      boff[nb] = tot;
+      *d_nnz = tot;
+    }
+  }
   hub_reservoir(a, ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6,
                 ((int64_t)gridDim.x * blockDim.x) >> 6);
 }
@@ -605,10 +618,12 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     DGS_HIP(hipMemsetAsync(d_nnz, 0, sizeof(int64_t), st));
     return;
   }
-  hipLaunchKernelGGL(k_scan_hop, dim3(1), dim3(kScanThreads), 0, st, bsum,
-                     bias_replace ? (const int64_t *)tsum : nullptr, Sc, boff, tboff, d_nnz,
-                     bsum + 2 * nb + 1);
-  DGS_LAUNCH_CHECK();
+  if (!use_hubs) {
+    hipLaunchKernelGGL(k_scan_hop, dim3(1), dim3(kScanThreads), 0, st, bsum,
+                       bias_replace ? (const int64_t *)tsum : nullptr, Sc, boff, tboff, d_nnz,
+                       bsum + 2 * nb + 1);
+    DGS_LAUNCH_CHECK();
+  }
 
   if (!bias) {
     DGS_CHECK(replace || k <= kMaxPicksLds, "num_picks > 512 is not supported without replacement");
@@ -617,7 +632,8 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     const size_t lds = replace ? 16 : sizeof(int32_t) * (size_t)kRowsPerBlock * k;
     const int64_t row_blocks = ceil_div(S, kRowsPerBlock);
     if (use_hubs) {
-      hipLaunchKernelGGL(k_hub_reservoir, dim3(kHubBlocks), dim3(256), 0, st, ua);
+      hipLaunchKernelGGL(k_hub_reservoir, dim3(kHubBlocks), dim3(256), 0, st, ua,
+                         (const int64_t *)bsum, boff, d_nnz);
       DGS_LAUNCH_CHECK();
     }
     if (replace)
