@@ -247,17 +247,19 @@ __device__ __forceinline__ void hub_reservoir(const UniformArgs &a, int64_t gw, 
         make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)(lane + 64), 0u), kk);
     // every d = idx + 1 of this chunk is >= k + 512 q + 1 (wave-uniform test)
     if (k + 512 * q + 1 >= (int64_t)kModBigMin && deg < (int64_t(1) << 30)) {
+      // 32-bit and branch-free up to the (rare) hit; a chunk entirely inside the row skips the
+      // bound test
+      const uint32_t b0 = (uint32_t)(k + 512 * q) + (uint32_t)lane;
+      const uint32_t deg32 = (uint32_t)deg, k32 = (uint32_t)k;
+      const bool full = k + 512 * q + 512 <= deg;
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
         const uint4 o4 = tt ? o4b : o4a;
-        const int64_t base = k + lane + 64 * tt + 512 * q;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-          const int64_t idx = base + 128 * w;
-          if (idx < deg) {
-            const uint32_t num = mod_big(u4_get(o4, w), (uint32_t)(idx + 1));
-            if ((int64_t)num < k) atomicMax(sl + num, (int32_t)idx);
-          }
+          const uint32_t idx = b0 + 64u * tt + 128u * w;
+          const uint32_t num = mod_big(u4_get(o4, w), idx + 1u);
+          if (num < k32 && (full || idx < deg32)) atomicMax(sl + num, (int32_t)idx);
         }
       }
     } else {
