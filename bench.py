@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--dim", type=int, default=100)
     p.add_argument("--shard", action="store_true",
                    help="cache node v on GPU v %% N (P2P over xGMI) instead of replicating")
+    p.add_argument("--bias", action="store_true",
+                   help="biased (degree-weighted) sampler: probs[e] = 1 + indeg(indices[e])")
     p.add_argument("--comm", choices=["gloo", "rccl"], default="gloo",
                    help="transport of the library's setup collectives in --shard mode")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
@@ -96,6 +98,11 @@ def main():
     gen.manual_seed(11)
     feats_d = torch.randn(N, args.dim, generator=gen, device=dev)
     labels_d = torch.randint(0, 47, (N,), generator=gen, device=dev)
+    probs = torch.Tensor()
+    if args.bias:  # degree-weighted, probs[e] = float32(1 + indeg(indices[e]))
+        indeg = torch.bincount(indices_d, minlength=indptr_d.numel() - 1)
+        probs = (1 + indeg[indices_d]).to(torch.float32).cpu()
+        del indeg
     indptr, indices = indptr_d.cpu(), indices_d.cpu()
     feats, labels = feats_d.cpu(), labels_d.cpu()
     del indptr_d, indices_d, feats_d, labels_d
@@ -112,7 +119,7 @@ def main():
     else:
         cache = torch.arange(N)
     t0 = time.time()
-    sampler = dgs.classes.P2PCacheSampler(indptr, indices, torch.Tensor(), cache, local_rank)
+    sampler = dgs.classes.P2PCacheSampler(indptr, indices, probs, cache, local_rank)
     server = dgs.classes.P2PCacheFeatureServer(feats, cache, local_rank)
     labels_dev = labels.to(dev)
     layout = server._layout()
@@ -188,7 +195,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(indptr, indices, feats, train, fan_out, args)
+        cpu = cpu_baseline(indptr, indices, probs if args.bias else None, feats, train, fan_out,
+                           args)
 
     out = {
         "metric": "sampled edges/sec + feature-gather GB/s, fan-out [15,10,5]",
@@ -205,7 +213,8 @@ def main():
         "data": "synthetic (RMAT a,b,c,d=.57,.19,.19,.05; randn f32 features; no OGB offline)",
         "config": {
             "workload": (f"products-like RMAT scale {args.scale} ef {args.ef} (N={N}, E={E}), "
-                         f"uniform sampler fan-out {fan_out} without replacement, B={args.batch} "
+                         f"{'biased (degree-weighted)' if args.bias else 'uniform'} sampler "
+                         f"fan-out {fan_out} without replacement, B={args.batch} "
                          f"seeds/step/GPU, + full-feature gather d={args.dim} f32 + label gather; "
                          + ("graph sharded v%N over GPUs (P2P)" if args.shard and world > 1
                             else "whole graph + features in HBM on every GPU")),
@@ -260,12 +269,14 @@ def seed_slice(train, rank, world):
     return train[rank * per:(rank + 1) * per]
 
 
-def cpu_baseline(indptr, indices, feats, train, fan_out, args):
-    """The oracle's OpenMP restatement on the host cores (DGL is not installed): uniform
-    row-wise sampling per hop + relabel + feature gather, same graph and batch size."""
+def cpu_baseline(indptr, indices, probs, feats, train, fan_out, args):
+    """The oracle's OpenMP restatement on the host cores (DGL is not installed): row-wise
+    sampling per hop (uniform, or biased when probs is given) + relabel + feature gather, same
+    graph and batch size."""
     from oracle import oracle as O
     threads = int(os.environ.get("DGS_CPU_THREADS", "16"))
     ip, ix = indptr.numpy(), indices.numpy()
+    pr = probs.numpy() if probs is not None else None
     fx = feats.numpy()
     rng = np.random.default_rng(1)
     seeds_all = train.numpy()
@@ -275,8 +286,12 @@ def cpu_baseline(indptr, indices, feats, train, fan_out, args):
         seeds = seeds_all[rng.integers(0, seeds_all.size, args.batch)]
         cur = seeds
         for h, k in enumerate(reversed(fan_out)):
-            r, c = O.sample_uniform(cur, ip, ix, k, False, 1000 + batches * 8 + h,
-                                    nthreads=threads)
+            if probs is None:
+                r, c = O.sample_uniform(cur, ip, ix, k, False, 1000 + batches * 8 + h,
+                                        nthreads=threads)
+            else:
+                r, c = O.sample_bias(cur, ip, ix, pr, k, False, 1000 + batches * 8 + h,
+                                     nthreads=threads)
             uniq, (rr, cc) = O.relabel([cur, c], [r, c])
             edges += c.size
             cur = uniq
@@ -289,7 +304,8 @@ def cpu_baseline(indptr, indices, feats, train, fan_out, args):
     return {"value": edges / dt, "unit": "sampled edges/s", "cores": threads, "kind": "port",
             "gather_GBps": rows * (2 * args.dim * 4 + 8) / dt / 1e9,
             "sample": (f"{batches} batches of B={args.batch}, fan-out {fan_out}, same graph; "
-                       f"oracle/dgs_oracle.c OpenMP sampler ({threads} threads) + serial relabel "
+                       f"oracle/dgs_oracle.c OpenMP {'biased' if probs is not None else 'uniform'} "
+                       f"sampler ({threads} threads) + serial relabel "
                        f"+ OpenMP gather, {dt:.1f}s")}
 
 

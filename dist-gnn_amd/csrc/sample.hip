@@ -28,6 +28,9 @@ constexpr int kTileRows = 256;   // rows per prep / sample workgroup
 constexpr int kGroup = 16;       // lanes per row in the uniform kernel
 constexpr int kRowsPerBlock = kTileRows / kGroup;  // rows per uniform-sampling workgroup
 constexpr int kHubT = 128;       // reservoir tail length above which a row goes to the hub kernel
+constexpr int kBiasHubT = 1024;  // biased rows above this degree are split across half-waves
+constexpr int kBiasChunk = 512;  // edges per biased hub chunk (32 lanes x 16 draws)
+constexpr int kBiasHubBlocks = 1024;  // workgroups of the biased hub kernel (8 half-waves each)
 constexpr int kHubBlocks = 2048; // workgroups of the hub kernel (8 waves per SIMD)
 constexpr int kMaxPicksLds = 512;
 constexpr int kScanThreads = 1024;
@@ -117,14 +120,19 @@ __global__ __launch_bounds__(kTileRows) void k_prep(RowSrc src, const int64_t *_
     tdeg = deg;
     if (use_hubs) {
       int64_t h = -1;
-      if (!replace && deg - k > kHubT) {
-        const uint64_t nch = (uint64_t)(deg - k + 511) / 512;
+      // 1: uniform hubs (reservoir tail > kHubT, 512-edge chunks); 2: biased hubs (degree >
+      // kBiasHubT, kBiasChunk-edge chunks)
+      const bool is_hub = use_hubs == 1 ? deg - k > kHubT : deg > kBiasHubT;
+      if (is_hub) {
+        const uint64_t nch = use_hubs == 1 ? (uint64_t)(deg - k + 511) / 512
+                                           : (uint64_t)(deg + kBiasChunk - 1) / kBiasChunk;
         const uint64_t old = atomicAdd((unsigned long long *)hub.count,
                                        (unsigned long long)((uint64_t(1) << kHubShift) | nch));
         h = (int64_t)(old >> kHubShift);
         hub.row[h] = i;
         hub.cptr[h] = (int64_t)(old & kHubChunkMask);
-        for (int64_t s2 = 0; s2 < k; ++s2) hubslot[h * k + s2] = (int32_t)s2;
+        if (use_hubs == 1)
+          for (int64_t s2 = 0; s2 < k; ++s2) hubslot[h * k + s2] = (int32_t)s2;
       }
       hub.hubid[i] = h;
     }
@@ -406,6 +414,20 @@ __device__ __forceinline__ float ares_key(float u, float p) {
 __device__ __forceinline__ bool ares_better(float ka, int64_t ia, float kb, int64_t ib) {
   return ka > kb || (ka == kb && ia < ib);
 }
+__device__ __forceinline__ bool ares_better(float ka, int32_t ia, float kb, int32_t ib) {
+  return ka > kb || (ka == kb && ia < ib);
+}
+
+// Cheap pre-test of the A-Res key against the current k-th best: an edge can only enter the top-k
+// if key = RN(log2f(u) / p) >= thr, which needs log2f(u) >= p * thr (p > 0, rounding aside).
+// The hardware log2 (v_log_f32) stands in for the fixed-operation log2 with slack (relative
+// 2^-16 of p * thr plus absolute 2^-16) far above both functions' error, so a rejected edge is
+// certainly not a candidate; survivors get the exact key.  Not used while thr is -inf.
+__device__ __forceinline__ bool ares_may_pass(float u, float p, float thr) {
+  if (!(p > 0.0f)) return false;
+  const float bound = p * thr;
+  return __builtin_amdgcn_logf(u) >= bound + bound * 0.0000152587890625f - 0.0000152587890625f;
+}
 
 // number of edges i < d with i = l (mod 32)
 __device__ __forceinline__ int64_t lane_draws(int64_t d, int l) {
@@ -425,12 +447,103 @@ __device__ __forceinline__ T float_max(T a, T b) {
 
 constexpr int kBiasRowsPerBlock = kTileRows / 32;  // one 32-lane half-wave per row
 
+// Half-wave top-k under the total order (key desc, edge index asc): lane q holds the q-th best
+// (key, idx) so far (a sorted list of 32; the first k count), thr = the k-th best.  A step's
+// candidates (one per lane) that beat thr are merged in one batch: bitonic sort of the 32
+// candidates, then a bitonic merge with the list (the reference's WarpSelect idea, on 32-lane
+// halves of a wave64).  Once the list is full almost no step has a candidate, so the common
+// cost is one compare and one ballot.
+struct HalfTopK {
+  float bk = -__builtin_inff();
+  int64_t bi = INT64_MAX;  // INT64_MAX: empty
+  int cnt = 0;
+  float thr_k = -__builtin_inff();
+  int64_t thr_i = INT64_MAX;
+  static __device__ __forceinline__ void cas(float &k, int64_t &i, int partner_mask, bool better_here) {
+    const float pk = __shfl_xor(k, partner_mask, 32);
+    const int64_t pi = __shfl_xor(i, partner_mask, 32);
+    const bool pb = ares_better(pk, pi, k, i);  // partner's entry is the better one
+    if (better_here ? pb : !pb) {
+      k = pk;
+      i = pi;
+    }
+  }
+  __device__ __forceinline__ void push(float key_i, int64_t i, bool valid, int64_t k, int l) {
+    const bool cand = valid && ares_better(key_i, i, thr_k, thr_i);
+    if (!half_ballot(cand)) return;
+    float ck = cand ? key_i : -__builtin_inff();
+    int64_t ci = cand ? i : INT64_MAX;
+    // bitonic sort of the candidates, descending
+#pragma unroll
+    for (int size = 2; size <= 32; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const bool desc = (l & size) == 0 || size == 32;
+        const bool lower = (l & stride) == 0;
+        cas(ck, ci, stride, desc == lower);
+      }
+    }
+    // top 32 of list + candidates: pairwise best against the reversed candidates (bitonic),
+    // then a descending bitonic merge
+    const float rk = __shfl(ck, 31 - l, 32);
+    const int64_t ri = __shfl(ci, 31 - l, 32);
+    if (ares_better(rk, ri, bk, bi)) {
+      bk = rk;
+      bi = ri;
+    }
+#pragma unroll
+    for (int stride = 16; stride > 0; stride >>= 1) cas(bk, bi, stride, (l & stride) == 0);
+    cnt = __builtin_popcount(half_ballot(l < k && bi != INT64_MAX));
+    thr_k = __shfl(bk, (int)(k - 1), 32);
+    thr_i = __shfl(bi, (int)(k - 1), 32);
+  }
+  // true once k entries are held and the threshold is finite (ares_may_pass is then valid)
+  __device__ __forceinline__ bool filtering(int64_t k) const {
+    return cnt >= k && thr_k > -__builtin_inff();
+  }
+};
+
+// A-Res candidates waiting to be merged: up to two per lane (u, p, edge).  An edge that passes
+// the cheap test is parked; the exact keys are computed and merged in one batch when some lane
+// would hold a third, or at the end -- so a merge absorbs many candidates instead of running
+// for every step with one.
+struct AresPending {
+  float u0 = 0.0f, p0 = 0.0f, u1 = 0.0f, p1 = 0.0f;
+  int64_t i0 = 0, i1 = 0;
+  bool h0 = false, h1 = false;
+  __device__ __forceinline__ void flush(HalfTopK &top, int64_t k, int l) {
+    if (half_ballot(h0)) top.push(h0 ? ares_key(u0, p0) : -__builtin_inff(), i0, h0, k, l);
+    if (half_ballot(h1)) top.push(h1 ? ares_key(u1, p1) : -__builtin_inff(), i1, h1, k, l);
+    h0 = h1 = false;
+  }
+  // edge i (valid) with draw u and weight p
+  __device__ __forceinline__ void add(float u, float p, int64_t i, bool valid, HalfTopK &top,
+                                      int64_t k, int l) {
+    const bool cand = valid && (!top.filtering(k) || ares_may_pass(u, p, top.thr_k));
+    if (half_ballot(cand && h0 && h1)) flush(top, k, l);
+    if (cand) {
+      if (!h0) {
+        u0 = u;
+        p0 = p;
+        i0 = i;
+        h0 = true;
+      } else {
+        u1 = u;
+        p1 = p;
+        i1 = i;
+        h1 = true;
+      }
+    }
+  }
+};
+
 template <bool kReplace>
 __global__ __launch_bounds__(kTileRows) void k_sample_bias(
     RowSrc src, Count Sc, int64_t k, uint64_t seed, const RowInfo *__restrict__ rowinfo,
     const int32_t *__restrict__ tpre, const int64_t *__restrict__ boff,
     const int32_t *__restrict__ tpre2, const int64_t *__restrict__ tboff, float *cdf,
-    int64_t *__restrict__ rowpos, int64_t *__restrict__ col, Table table) {
+    int64_t *__restrict__ rowpos, int64_t *__restrict__ col, Table table,
+    const int64_t *__restrict__ hubid) {
   const int64_t S = Sc.get();
   const int64_t G = (S + 15) / 16;  // reference grid: ceil(S / TILE_SIZE=16)
   const int hw = threadIdx.x >> 5, l = threadIdx.x & 31;
@@ -468,17 +581,14 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
         }
         return;
       }
-      // half-wave top-k: lane q holds the q-th best (key, idx) so far
-      float bk = -__builtin_inff();
-      int64_t bi = INT64_MAX;
-      int cnt = 0;
-      float thr_k = 0.0f;
-      int64_t thr_i = 0;
+      if (hubid && hubid[r] >= 0) return;  // split across half-waves: k_bias_hub / _merge
+      HalfTopK top;
       uint4 o4 = make_uint4(0, 0, 0, 0);
       int64_t cached_q = -1;
+      AresPending pend;
       for (int64_t base = 0; base < deg; base += 32) {
         const int64_t i = base + l;
-        float key_i = -__builtin_inff();
+        float u = 0.0f, pv = 0.0f;
         if (i < deg) {
           const int64_t q = j >> 2;
           if (q != cached_q) {
@@ -486,39 +596,15 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
                                kk);
             cached_q = q;
           }
-          const float u = curand_uniform_from(u4_get(o4, (int)(j & 3)));
-          key_i = ares_key(u, pr[i]);
+          u = curand_uniform_from(u4_get(o4, (int)(j & 3)));
+          pv = pr[i];
           ++j;
         }
-        bool cand = i < deg && (cnt < k || ares_better(key_i, i, thr_k, thr_i));
-        uint32_t mask = half_ballot(cand);
-        while (mask) {
-          const int c = __builtin_ctz(mask);
-          const float ck = __shfl(key_i, c, 32);
-          const int64_t ci = __shfl(i, c, 32);
-          const uint32_t better = half_ballot(l < cnt && ares_better(bk, bi, ck, ci));
-          const int pos = __builtin_popcount(better);
-          const float nk = __shfl_up(bk, 1, 32);
-          const int64_t ni = __shfl_up(bi, 1, 32);
-          if (pos < k) {
-            if (l > pos) {
-              bk = nk;
-              bi = ni;
-            } else if (l == pos) {
-              bk = ck;
-              bi = ci;
-            }
-            if (cnt < k) ++cnt;
-          }
-          thr_k = __shfl(bk, (int)(k - 1), 32);
-          thr_i = __shfl(bi, (int)(k - 1), 32);
-          mask &= ~(1u << c);
-          cand = cand && (l != c) && (cnt < k || ares_better(key_i, i, thr_k, thr_i));
-          mask &= half_ballot(cand);
-        }
+        pend.add(u, pv, i, i < deg, top, k, l);
       }
+      pend.flush(top, k, l);
       if (l < k) {
-        const int64_t v = nb[bi];
+        const int64_t v = nb[top.bi];
         rowpos[out + l] = r;
         col[out + l] = v;
         table_record(table, v, S + out + l);
@@ -576,6 +662,206 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Biased hub rows (A-Res without replacement, degree > kBiasHubT).  Edge i of a row draws
+// curand number j = c_l + i / 32 of subsequence 32w + l (l = i % 32; c_l = draws lane l made on
+// the chain's earlier rows), so any half-wave can evaluate any edge's key.  Half-wave workers
+// take contiguous ranges of kBiasChunk-edge chunks over the hub list, keep a running top-k per
+// row and flush it to slot (worker + hub) -- unique, since the (worker, hub) pairs a static
+// partition visits form a staircase -- and k_bias_hub_merge reduces each row's slots.
+struct BiasHubArgs {
+  RowSrc src;
+  Count Sc;
+  int64_t k;
+  uint64_t seed;
+  const RowInfo *rowinfo;
+  const int32_t *tpre;
+  const int64_t *boff;
+  HubView hub;
+  float *ckey;
+  int32_t *cidx;
+  int32_t *ccnt;
+  int32_t *wfirst;  // per hub row: workers holding its first / last chunk
+  int32_t *wlast;
+  int64_t nworkers;
+  int64_t *rowpos;
+  int64_t *col;
+  Table table;
+};
+
+// draws lane l made on the earlier rows of row r's (block, warp) chain (no replacement)
+__device__ __forceinline__ int64_t chain_draws(const RowInfo *rowinfo, int64_t r, int64_t k,
+                                               int l) {
+  const int64_t b = r / 16;
+  const int w = (int)((r % 16) & 3), m = (int)((r % 16) >> 2);
+  int64_t j = 0;
+  for (int mm = 0; mm < m; ++mm) {
+    const int64_t d = ri_deg(rowinfo[b * 16 + w + 4 * mm]);
+    if (d > k) j += lane_draws(d, l);
+  }
+  return j;
+}
+
+__device__ __forceinline__ int64_t bias_worker_c0(int64_t total, int64_t w, int64_t nw) {
+  return total * w / nw;
+}
+
+// Workers actually used: at least 4 chunks each, so a row's chunks meet few workers (few
+// partial lists to merge); both kernels derive it from the same device-side total.
+__device__ __forceinline__ int64_t bias_workers(int64_t total, int64_t max_workers) {
+  const int64_t w = total / 4;
+  return w < 1 ? 1 : (w > max_workers ? max_workers : w);
+}
+
+__global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
+  const int64_t S = a.Sc.get();
+  const int64_t G = (S + 15) / 16;
+  const uint64_t packed = (uint64_t)*a.hub.count;
+  const int64_t H = (int64_t)(packed >> kHubShift);
+  if (H == 0) return;
+  const int64_t total = (int64_t)(packed & kHubChunkMask);
+  const int l = threadIdx.x & 31;
+  const int64_t wk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 5;
+  const int64_t nw = bias_workers(total, a.nworkers);
+  if (wk >= nw) return;
+  const int64_t c0 = bias_worker_c0(total, wk, nw);
+  const int64_t c1 = bias_worker_c0(total, wk + 1, nw);
+  if (c0 >= c1) return;
+  const int64_t k = a.k;
+  int64_t lo = 0, hi = H;  // largest h with cptr[h] <= c0
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a.hub.cptr[mid] <= c0) lo = mid; else hi = mid;
+  }
+  int64_t h = lo;
+  int64_t hstart = 0, hnext = 0, deg = 0, jb = 0;
+  const float *pr = nullptr;
+  uint2 kk;
+  uint32_t sub = 0;
+  HalfTopK top;
+  auto load_row = [&](int64_t hh) {
+    hstart = a.hub.cptr[hh];
+    hnext = hh + 1 < H ? a.hub.cptr[hh + 1] : total;
+    const int64_t r = a.hub.row[hh];
+    const RowInfo ri = a.rowinfo[r];
+    deg = ri_deg(ri);
+    pr = row_probs(a.src, ri);
+    const uint64_t key = a.seed * (uint64_t)G + (uint64_t)(r / 16);
+    kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
+    sub = (uint32_t)(32 * ((r % 16) & 3) + l);
+    jb = chain_draws(a.rowinfo, r, k, l);
+    top = HalfTopK();
+  };
+  AresPending pend;
+  auto flush = [&](int64_t hh) {
+    pend.flush(top, k, l);
+    const int64_t slot = wk + hh;
+    if (l < top.cnt) {
+      a.ckey[slot * k + l] = top.bk;
+      a.cidx[slot * k + l] = (int32_t)top.bi;
+    }
+    if (l == 0) a.ccnt[slot] = top.cnt;
+  };
+  load_row(h);
+  constexpr int kT = kBiasChunk / 32;
+  for (int64_t c = c0; c < c1; ++c) {
+    while (c >= hnext) {
+      flush(h);
+      ++h;
+      load_row(h);
+    }
+    const int64_t q = c - hstart;
+    if (l == 0 && c == hstart) a.wfirst[h] = (int32_t)wk;
+    if (l == 0 && c == hnext - 1) a.wlast[h] = (int32_t)wk;
+    const int64_t i0 = q * kBiasChunk + l;
+    float p[kT];
+#pragma unroll
+    for (int t = 0; t < kT; ++t) {
+      const int64_t i = i0 + 32 * t;
+      p[t] = pr[i < deg ? i : deg - 1];
+    }
+    // this lane's 16 draws j = jb + 16q + t lie in 5 consecutive Philox blocks: compute all
+    // five (uniform control flow -- lanes' chain offsets differ, a lazy per-lane refill would
+    // diverge into a Philox per step) and select draw t as word off + t
+    const int64_t j0 = jb + q * kT;
+    const int64_t cb = j0 >> 2;
+    const int off = (int)(j0 & 3);
+    uint32_t wv[4 * (kT / 4 + 1)];
+#pragma unroll
+    for (int bq = 0; bq < kT / 4 + 1; ++bq) {
+      const uint64_t cq = (uint64_t)(cb + bq);
+      const uint4 o = philox4x32_10(make_uint4((uint32_t)cq, (uint32_t)(cq >> 32), sub, 0u), kk);
+      wv[4 * bq + 0] = o.x;
+      wv[4 * bq + 1] = o.y;
+      wv[4 * bq + 2] = o.z;
+      wv[4 * bq + 3] = o.w;
+    }
+#pragma unroll
+    for (int t = 0; t < kT; ++t) {
+      const int64_t i = i0 + 32 * t;
+      uint32_t x = wv[t];
+      x = off == 1 ? wv[t + 1] : x;
+      x = off == 2 ? wv[t + 2] : x;
+      x = off == 3 ? wv[t + 3] : x;
+      const float u = curand_uniform_from(x);
+      pend.add(u, p[t], i, i < deg, top, k, l);
+    }
+  }
+  flush(h);
+}
+
+// One workgroup per hub row: its 8 half-waves reduce interleaved subsets of the row's worker
+// slots, then half-wave 0 merges the 8 partial lists and emits the picks.
+__global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
+  __shared__ float s_key[8][32];
+  __shared__ int64_t s_idx[8][32];
+  __shared__ int s_cnt[8];
+  const int64_t S = a.Sc.get();
+  const uint64_t packed = (uint64_t)*a.hub.count;
+  const int64_t H = (int64_t)(packed >> kHubShift);
+  const int64_t total = (int64_t)(packed & kHubChunkMask);
+  const int64_t nw = bias_workers(total, a.nworkers);
+  const int64_t k = a.k;
+  const int l = threadIdx.x & 31, g = threadIdx.x >> 5;
+  for (int64_t h = blockIdx.x; h < H; h += gridDim.x) {
+    const int64_t wf = a.wfirst[h], wl = a.wlast[h];
+    HalfTopK top;
+    for (int64_t w = wf + g; w <= wl; w += 8) {
+      if (bias_worker_c0(total, w, nw) == bias_worker_c0(total, w + 1, nw)) continue;  // empty
+      const int64_t slot = w + h;
+      const int n = a.ccnt[slot];
+      float key_i = -__builtin_inff();
+      int64_t i = INT64_MAX;
+      if (l < n) {
+        key_i = a.ckey[slot * k + l];
+        i = a.cidx[slot * k + l];
+      }
+      top.push(key_i, i, l < n, k, l);
+    }
+    s_key[g][l] = top.bk;
+    s_idx[g][l] = top.bi;
+    if (l == 0) s_cnt[g] = top.cnt;
+    __syncthreads();
+    if (g == 0) {
+      HalfTopK fin;
+      for (int gg = 0; gg < 8; ++gg) {
+        const int n = s_cnt[gg];
+        fin.push(s_key[gg][l], s_idx[gg][l], l < n, k, l);
+      }
+      const int64_t r = a.hub.row[h];
+      const RowInfo ri = a.rowinfo[r];
+      const int64_t out = a.boff[r / kTileRows] + a.tpre[r];
+      if (l < k) {
+        const int64_t v = ri.ptr[fin.bi];
+        a.rowpos[out + l] = r;
+        a.col[out + l] = v;
+        table_record(a.table, v, S + out + l);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------
@@ -599,6 +885,7 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     return;
   }
   const bool use_hubs = !bias && !replace && k > 0 && S < kHubMaxRows;
+  const bool bias_hubs = bias && !replace && k > 0 && S < kHubMaxRows;
   // Two hub counters used by alternate hops (a global hop serial, so calls chain correctly):
   // each prep zeroes the other one; zeroed once at allocation.
   if (ws.hubcount.ensure(128)) DGS_HIP(hipMemsetAsync(ws.hubcount.p, 0, 128, st));
@@ -613,7 +900,8 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   int32_t *tpre2 = tpre + S;
   if (use_hubs) ws.hubslot.ensure(sizeof(int32_t) * (size_t)(S * k));
   hipLaunchKernelGGL(k_prep, dim3((unsigned)nb), dim3(kTileRows), 0, st, src, seeds, Sc, k,
-                     (int)replace, (int)use_hubs, (int)bias_replace, rowinfo, tpre, tpre2, bsum,
+                     (int)replace, use_hubs ? 1 : (bias_hubs ? 2 : 0), (int)bias_replace, rowinfo,
+                     tpre, tpre2, bsum,
                      tsum, hub, ws.hubslot.as<int32_t>(), table, next_count);
   DGS_LAUNCH_CHECK();
   if (k == 0) {  // seeds still enter the relabel table (frontier = unique(seeds))
@@ -649,6 +937,21 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     DGS_CHECK(k <= 32, "biased sampling supports num_picks <= 32 (rowwise_sampling_bias.cu:73)");
     float *cdf = nullptr;
     const dim3 grid((unsigned)ceil_div(S, kBiasRowsPerBlock));
+    const int64_t nworkers = (int64_t)kBiasHubBlocks * (kTileRows / 32);
+    BiasHubArgs ba{};
+    if (bias_hubs) {
+      const int64_t slots = nworkers + S;
+      ws.cand.ensure((sizeof(float) + sizeof(int32_t)) * (size_t)(slots * k) +
+                     sizeof(int32_t) * (size_t)(slots + 2 * S));
+      float *ckey = ws.cand.as<float>();
+      int32_t *cidx = reinterpret_cast<int32_t *>(ckey + slots * k);
+      int32_t *ccnt = cidx + slots * k;
+      int32_t *wfirst = ccnt + slots;
+      ba = BiasHubArgs{src, Sc, k, launch_seed, rowinfo, tpre, boff, hub, ckey, cidx, ccnt,
+                       wfirst, wfirst + S, nworkers, rowpos, col, table};
+      hipLaunchKernelGGL(k_bias_hub, dim3(kBiasHubBlocks), dim3(kTileRows), 0, st, ba);
+      DGS_LAUNCH_CHECK();
+    }
     if (replace) {
       // CDF scratch = sum of degrees (the reference's temp tensor, :257-259): one D2H.
       int64_t *h = (ws.host.ensure(64), ws.host.as<int64_t>() + 4);
@@ -657,12 +960,19 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
       ws.cdf.ensure(sizeof(float) * (size_t)(h[0] > 0 ? h[0] : 1));
       cdf = ws.cdf.as<float>();
       hipLaunchKernelGGL(k_sample_bias<true>, grid, dim3(kTileRows), 0, st, src, Sc, k,
-                         launch_seed, rowinfo, tpre, boff, tpre2, tboff, cdf, rowpos, col, table);
+                         launch_seed, rowinfo, tpre, boff, tpre2, tboff, cdf, rowpos, col, table,
+                         (const int64_t *)nullptr);
     } else {
       hipLaunchKernelGGL(k_sample_bias<false>, grid, dim3(kTileRows), 0, st, src, Sc, k,
-                         launch_seed, rowinfo, tpre, boff, tpre2, tboff, cdf, rowpos, col, table);
+                         launch_seed, rowinfo, tpre, boff, tpre2, tboff, cdf, rowpos, col, table,
+                         bias_hubs ? (const int64_t *)hub.hubid : nullptr);
     }
     DGS_LAUNCH_CHECK();
+    if (bias_hubs) {
+      hipLaunchKernelGGL(k_bias_hub_merge, dim3((unsigned)std::min<int64_t>(S, 2048)),
+                         dim3(kTileRows), 0, st, ba);
+      DGS_LAUNCH_CHECK();
+    }
   }
 }
 

@@ -378,71 +378,106 @@ static void build_cdf(const float *p, int64_t deg, float *cdf) {
   }
 }
 
-int64_t oracle_sample_bias(const int64_t *seeds, int64_t S, const int64_t *indptr,
-                           const int64_t *indices, const float *probs, int64_t k, int replace,
-                           uint64_t launch_seed, int64_t *out_row, int64_t *out_col) {
-  int64_t *offs = (int64_t *)malloc(sizeof(int64_t) * (size_t)(S + 1));
-  offs[0] = 0;
-  int64_t max_deg = 0;
-  for (int64_t r = 0; r < S; r++) {
-    int64_t row = seeds[r];
-    int64_t deg = indptr[row + 1] - indptr[row];
-    if (deg > max_deg) max_deg = deg;
-    offs[r + 1] = offs[r] + row_count(deg, k, replace);
-  }
-  const int64_t G = (S + 15) / 16;
-  ares_entry *buf = (ares_entry *)malloc(sizeof(ares_entry) * (size_t)(k > 0 ? k : 1));
-  float *cdf = (float *)malloc(sizeof(float) * (size_t)(max_deg > 0 ? max_deg : 1));
+/* One 16-row block b of K5 / K6 (4 warp chains of rows b*16 + w + 4m).  buf: k entries,
+ * cdf: max_deg floats (scratch of the calling thread). */
+static void sample_bias_block(int64_t b, const int64_t *seeds, int64_t S, int64_t G,
+                              const int64_t *indptr, const int64_t *indices, const float *probs,
+                              int64_t k, int replace, uint64_t launch_seed, const int64_t *offs,
+                              int64_t *out_row, int64_t *out_col, ares_entry *buf, float *cdf) {
   oracle_philox_t st[32];
-  for (int64_t b = 0; b < G; b++) {
-    const uint64_t key = launch_seed * (uint64_t)G + (uint64_t)b;
-    const int64_t last_row = (b + 1) * 16 < S ? (b + 1) * 16 : S;
-    for (int w = 0; w < 4; w++) {
-      for (int l = 0; l < 32; l++)
-        oracle_curand_init(key, replace ? (uint64_t)(4 * w + l) : (uint64_t)(32 * w + l), 0,
-                           &st[l]);
-      for (int64_t r = b * 16 + w; r < last_row; r += 4) {
-        const int64_t row = seeds[r];
-        const int64_t begin = indptr[row];
-        const int64_t deg = indptr[row + 1] - begin;
-        const int64_t o = offs[r];
-        if (!replace) {
-          if (deg > k) {
-            int64_t cnt = 0;
-            for (int64_t i = 0; i < deg; i++) {
-              float u = oracle_curand_uniform(&st[i % 32]);
-              float key_i = oracle_ares_key(u, probs[begin + i]);
-              topk_insert(buf, &cnt, k, key_i, i);
-            }
-            for (int64_t j = 0; j < k; j++) {
-              out_row[o + j] = row;
-              out_col[o + j] = indices[begin + buf[j].idx];
-            }
-          } else {
-            for (int64_t i = 0; i < deg; i++) {
-              out_row[o + i] = row;
-              out_col[o + i] = indices[begin + i];
-            }
+  const uint64_t key = launch_seed * (uint64_t)G + (uint64_t)b;
+  const int64_t last_row = (b + 1) * 16 < S ? (b + 1) * 16 : S;
+  for (int w = 0; w < 4; w++) {
+    for (int l = 0; l < 32; l++)
+      oracle_curand_init(key, replace ? (uint64_t)(4 * w + l) : (uint64_t)(32 * w + l), 0,
+                         &st[l]);
+    for (int64_t r = b * 16 + w; r < last_row; r += 4) {
+      const int64_t row = seeds[r];
+      const int64_t begin = indptr[row];
+      const int64_t deg = indptr[row + 1] - begin;
+      const int64_t o = offs[r];
+      if (!replace) {
+        if (deg > k) {
+          int64_t cnt = 0;
+          for (int64_t i = 0; i < deg; i++) {
+            float u = oracle_curand_uniform(&st[i % 32]);
+            float key_i = oracle_ares_key(u, probs[begin + i]);
+            topk_insert(buf, &cnt, k, key_i, i);
           }
-        } else if (deg > 0) {
-          build_cdf(probs + begin, deg, cdf);
-          const float sum = cdf[deg - 1];
-          for (int64_t idx = 0; idx < k; idx++) {
-            float u = oracle_curand_uniform(&st[idx % 32]);
-            float rnd = u * sum;
-            int64_t item = cub_upper_bound(cdf, deg, rnd);
-            if (item > deg - 1) item = deg - 1;
-            out_row[o + idx] = row;
-            out_col[o + idx] = indices[begin + item];
+          for (int64_t j = 0; j < k; j++) {
+            out_row[o + j] = row;
+            out_col[o + j] = indices[begin + buf[j].idx];
           }
+        } else {
+          for (int64_t i = 0; i < deg; i++) {
+            out_row[o + i] = row;
+            out_col[o + i] = indices[begin + i];
+          }
+        }
+      } else if (deg > 0) {
+        build_cdf(probs + begin, deg, cdf);
+        const float sum = cdf[deg - 1];
+        for (int64_t idx = 0; idx < k; idx++) {
+          float u = oracle_curand_uniform(&st[idx % 32]);
+          float rnd = u * sum;
+          int64_t item = cub_upper_bound(cdf, deg, rnd);
+          if (item > deg - 1) item = deg - 1;
+          out_row[o + idx] = row;
+          out_col[o + idx] = indices[begin + item];
         }
       }
     }
   }
+}
+
+/* offs[0..S] (output offsets) and the largest degree among the seeds */
+static int64_t *bias_offsets(const int64_t *seeds, int64_t S, const int64_t *indptr, int64_t k,
+                             int replace, int64_t *max_deg) {
+  int64_t *offs = (int64_t *)malloc(sizeof(int64_t) * (size_t)(S + 1));
+  offs[0] = 0;
+  *max_deg = 0;
+  for (int64_t r = 0; r < S; r++) {
+    int64_t row = seeds[r];
+    int64_t deg = indptr[row + 1] - indptr[row];
+    if (deg > *max_deg) *max_deg = deg;
+    offs[r + 1] = offs[r] + row_count(deg, k, replace);
+  }
+  return offs;
+}
+
+int64_t oracle_sample_bias(const int64_t *seeds, int64_t S, const int64_t *indptr,
+                           const int64_t *indices, const float *probs, int64_t k, int replace,
+                           uint64_t launch_seed, int64_t *out_row, int64_t *out_col) {
+  return oracle_sample_bias_omp(seeds, S, indptr, indices, probs, k, replace, launch_seed,
+                                out_row, out_col, 1);
+}
+
+/* Blocks are independent RNG streams (key = seed * G + b), so they run in parallel. */
+int64_t oracle_sample_bias_omp(const int64_t *seeds, int64_t S, const int64_t *indptr,
+                               const int64_t *indices, const float *probs, int64_t k,
+                               int replace, uint64_t launch_seed, int64_t *out_row,
+                               int64_t *out_col, int nthreads) {
+  int64_t max_deg = 0;
+  int64_t *offs = bias_offsets(seeds, S, indptr, k, replace, &max_deg);
+  const int64_t G = (S + 15) / 16;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads > 0 ? nthreads : omp_get_max_threads())
+#endif
+  {
+    ares_entry *buf = (ares_entry *)malloc(sizeof(ares_entry) * (size_t)(k > 0 ? k : 1));
+    float *cdf = (float *)malloc(sizeof(float) * (size_t)(max_deg > 0 ? max_deg : 1));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 4)
+#endif
+    for (int64_t b = 0; b < G; b++)
+      sample_bias_block(b, seeds, S, G, indptr, indices, probs, k, replace, launch_seed, offs,
+                        out_row, out_col, buf, cdf);
+    free(buf);
+    free(cdf);
+  }
   int64_t nnz = offs[S];
   free(offs);
-  free(buf);
-  free(cdf);
+  (void)nthreads;
   return nnz;
 }
 

@@ -110,6 +110,10 @@ int64_t oracle_sample_uniform_omp(const int64_t *seeds, int64_t S, const int64_t
                                   const int64_t *indices, int64_t k, int replace,
                                   uint64_t launch_seed, int64_t *out_row, int64_t *out_col,
                                   int nthreads);
+int64_t oracle_sample_bias_omp(const int64_t *seeds, int64_t S, const int64_t *indptr,
+                               const int64_t *indices, const float *probs, int64_t k,
+                               int replace, uint64_t launch_seed, int64_t *out_row,
+                               int64_t *out_col, int nthreads);
 int oracle_max_threads(void);
 
 #ifdef __cplusplus

@@ -47,7 +47,7 @@ def lib():
         L.oracle_curand_init.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                          ctypes.c_void_p]
         for name in ("oracle_sample_uniform", "oracle_sample_bias", "oracle_relabel",
-                     "oracle_sample_uniform_omp"):
+                     "oracle_sample_uniform_omp", "oracle_sample_bias_omp"):
             getattr(L, name).restype = ctypes.c_int64
         L.oracle_max_threads.restype = ctypes.c_int
         _lib = L
@@ -133,15 +133,16 @@ def sample_uniform(seeds, indptr, indices, k, replace, launch_seed, nthreads=1):
     return row[:nnz].copy(), col[:nnz].copy()
 
 
-def sample_bias(seeds, indptr, indices, probs, k, replace, launch_seed):
+def sample_bias(seeds, indptr, indices, probs, k, replace, launch_seed, nthreads=1):
     seeds, indptr, indices = _i64(seeds), _i64(indptr), _i64(indices)
     probs = np.ascontiguousarray(np.asarray(probs, dtype=np.float32))
     S = seeds.size
     cap = max(S * k, 1)
     row = np.empty(cap, np.int64)
     col = np.empty(cap, np.int64)
-    nnz = lib().oracle_sample_bias(_p(seeds), S, _p(indptr), _p(indices), _p(probs, _f32p), k,
-                                   int(replace), ctypes.c_uint64(launch_seed), _p(row), _p(col))
+    nnz = lib().oracle_sample_bias_omp(_p(seeds), S, _p(indptr), _p(indices), _p(probs, _f32p),
+                                       k, int(replace), ctypes.c_uint64(launch_seed), _p(row),
+                                       _p(col), int(nthreads))
     return row[:nnz].copy(), col[:nnz].copy()
 
 
