@@ -26,14 +26,27 @@ def per_kernel(path_glob, counter, kernel_re):
     return vals
 
 
+def kernel_names(path_glob):
+    names = set()
+    for path in glob.glob(path_glob, recursive=True):
+        for r in csv.DictReader(open(path)):
+            names.add(r.get("Kernel_Name", ""))
+    return names
+
+
 def main(root):
-    table_re = r"k_gather<16, dgs::\(anonymous namespace\)::TableSrc>"
+    # the feature-server gather: computed addresses (StridedSrc, whole graph cached) or the
+    # address-table form (TableSrc)
+    table_re = r"k_gather<16, dgs::\(anonymous namespace\)::(TableSrc|StridedSrc<\w+>) ?>"
     plain_re = r"k_gather<16, dgs::\(anonymous namespace\)::PlainSrc<long> >"
     bf = per_kernel(f"{root}/pmc_bench_fetch/**/*counter_collection.csv", "FETCH_SIZE", table_re)
     bw = per_kernel(f"{root}/pmc_bench_write/**/*counter_collection.csv", "WRITE_SIZE", table_re)
     cf = per_kernel(f"{root}/pmc_calib_fetch/**/*counter_collection.csv", "FETCH_SIZE", plain_re)
     cw = per_kernel(f"{root}/pmc_calib_write/**/*counter_collection.csv", "WRITE_SIZE", plain_re)
     assert bf and bw and cf and cw, (len(bf), len(bw), len(cf), len(cw))
+    kernel_name = "k_gather<16, StridedSrc>" if any(
+        "StridedSrc" in n for n in kernel_names(f"{root}/pmc_bench_fetch/**/*counter_collection.csv")
+    ) else "k_gather<16, TableSrc>"
     N, D = 1 << 22, 100
     calib_read = N * (D * 4 + 8)          # rows + nids
     calib_write = N * D * 4
@@ -42,10 +55,15 @@ def main(root):
     read_factor = calib_read / cfetch
     write_factor = calib_write / cwrite
     bench_rows = float(os.environ.get("BENCH_ROWS_PER_LAUNCH", "0"))
+    line = glob.glob(f"{root}/pmc_bench_fetch.log")
+    if not bench_rows and line:
+        for ln in open(line[0]):
+            if ln.startswith("{"):
+                bench_rows = json.loads(ln)["gathered_rows_per_step"]
     fetch = sum(bf) / len(bf) * 1024 * read_factor
     write = sum(bw) / len(bw) * 1024 * write_factor
     out = {
-        "kernel": "k_gather<16, TableSrc>", "dim": D,
+        "kernel": kernel_name, "dim": D,
         "calibration": {"workload": "sequential gather of 2^22 rows x 400 B (tools/gather_calib.py)",
                         "expected_read_bytes": calib_read, "fetch_size_bytes": cfetch,
                         "read_factor": read_factor, "expected_write_bytes": calib_write,
