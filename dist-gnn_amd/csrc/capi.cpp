@@ -240,7 +240,23 @@ int dgs_compute_frontier_heat(const int64_t *seeds, int64_t n_seeds, const int64
     DGS_HIP(hipMemsetAsync(frontier_heat, 0, sizeof(float) * (size_t)num_nodes, st));
     heat(dev_ptr(seeds, "seeds"), n_seeds, dev_ptr(indptr, "indptr"),
          dev_ptr(indices, "indices"), dev_ptr(probs, "probs"), dev_ptr(seeds_heat, "seeds_heat"),
-         num_picks, indptr_diff, frontier_heat, st);
+         num_picks, indptr_diff, frontier_heat, num_nodes, nullptr, st);
+  });
+}
+
+int dgs_compute_frontier_heat_fixed(const int64_t *seeds, int64_t n_seeds,
+                                    const int64_t *indptr, const int64_t *indices,
+                                    const float *probs, const float *seeds_heat,
+                                    int64_t num_nodes, int64_t num_picks, int64_t indptr_diff,
+                                    float *frontier_heat, void *stream) {
+  return guard([&] {
+    hipStream_t st = S(stream);
+    HopScratch &ws = op_scratch();
+    ws.misc.ensure(sizeof(uint64_t) * (size_t)(num_nodes > 0 ? num_nodes : 1));
+    heat(dev_ptr(seeds, "seeds"), n_seeds, dev_ptr(indptr, "indptr"),
+         dev_ptr(indices, "indices"), dev_ptr(probs, "probs"), dev_ptr(seeds_heat, "seeds_heat"),
+         num_picks, indptr_diff, frontier_heat, num_nodes, ws.misc.as<unsigned long long>(),
+         st);
   });
 }
 

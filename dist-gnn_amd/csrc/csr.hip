@@ -63,10 +63,27 @@ __global__ void k_ntab_assign(NodeEntry *ntab, const int64_t *nids, const int64_
   }
 }
 
-// preprocess_heat.cu:14-33 -- one thread per seed, float atomics into frontier_heat.
+// Heat accumulation: float atomics as the reference (order-dependent rounding), or fixed point
+// (deterministic): messages are rounded to multiples of 2^-36 and summed as int64, which is
+// associative, so the result does not depend on the order the atomics land in.  Resolution
+// 1.5e-11; no overflow below 2^27 unit messages into one node.
+constexpr double kHeatFixedScale = 68719476736.0;  // 2^36
+struct FloatHeat {
+  float *fh;
+  __device__ __forceinline__ void add(int64_t v, float m) const { atomicAdd(fh + v, m); }
+};
+struct FixedHeat {
+  unsigned long long *acc;
+  __device__ __forceinline__ void add(int64_t v, float m) const {
+    atomicAdd(acc + v, (unsigned long long)__double2ll_rn((double)m * kHeatFixedScale));
+  }
+};
+
+// preprocess_heat.cu:14-33 -- one thread per seed; message min(1, heat * k / deg) per edge.
+template <typename Acc>
 __global__ void k_heat(const int64_t *seeds, int64_t n, const int64_t *indptr,
                        const int64_t *indices, const float *seeds_heat, int64_t num_picks,
-                       int64_t indptr_diff, float *fh) {
+                       int64_t indptr_diff, Acc acc) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
   const int64_t row = seeds[s];
@@ -75,13 +92,14 @@ __global__ void k_heat(const int64_t *seeds, int64_t n, const int64_t *indptr,
   if (deg <= 0) return;
   const float m = __fdiv_rn(__fmul_rn(seeds_heat[row], (float)num_picks), (float)deg);
   const float msg = (1.0f < m) ? 1.0f : m;
-  for (int64_t i = b; i < e; ++i) atomicAdd(fh + indices[i], msg);
+  for (int64_t i = b; i < e; ++i) acc.add(indices[i], msg);
 }
 
 // preprocess_heat.cu:58-98 -- the biased variant; row probabilities summed in edge order.
+template <typename Acc>
 __global__ void k_heat_bias(const int64_t *seeds, int64_t n, const int64_t *indptr,
                             const int64_t *indices, const float *probs, const float *seeds_heat,
-                            int64_t num_picks, int64_t indptr_diff, float *fh) {
+                            int64_t num_picks, int64_t indptr_diff, Acc acc) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
   const int64_t row = seeds[s];
@@ -92,8 +110,13 @@ __global__ void k_heat_bias(const int64_t *seeds, int64_t n, const int64_t *indp
   for (int64_t i = b; i < e; ++i) {
     const float m = __fmul_rn(hk, __fdiv_rn(probs[i], psum));
     const float msg = (1.0f < m) ? 1.0f : m;
-    atomicAdd(fh + indices[i], msg);
+    acc.add(indices[i], msg);
   }
+}
+
+__global__ void k_heat_fixed_to_float(const unsigned long long *acc, int64_t n, float *fh) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < n) fh[v] = (float)((double)(long long)acc[v] / kHeatFixedScale);
 }
 
 __global__ void k_cached_flag(const int64_t *tab, int64_t n, int64_t *flag) {
@@ -191,17 +214,36 @@ void ntab_assign(NodeEntry *ntab, const int64_t *nids, const int64_t *sub_indptr
 
 void heat(const int64_t *seeds, int64_t n_seeds, const int64_t *indptr, const int64_t *indices,
           const float *probs, const float *seeds_heat, int64_t num_picks, int64_t indptr_diff,
-          float *frontier_heat, hipStream_t st) {
+          float *frontier_heat, int64_t num_nodes, unsigned long long *fixed_acc,
+          hipStream_t st) {
   if (probs) n_seeds -= 1;  // preprocess_heat.cu:107 processes seeds.numel() - 1 seeds
-  if (n_seeds <= 0) return;
-  const dim3 grid((unsigned)ceil_div(n_seeds, 128)), block(128);
-  if (probs)
-    hipLaunchKernelGGL(k_heat_bias, grid, block, 0, st, seeds, n_seeds, indptr, indices, probs,
-                       seeds_heat, num_picks, indptr_diff, frontier_heat);
-  else
-    hipLaunchKernelGGL(k_heat, grid, block, 0, st, seeds, n_seeds, indptr, indices, seeds_heat,
-                       num_picks, indptr_diff, frontier_heat);
-  DGS_LAUNCH_CHECK();
+  if (fixed_acc) DGS_HIP(hipMemsetAsync(fixed_acc, 0, sizeof(uint64_t) * (size_t)num_nodes, st));
+  if (n_seeds > 0) {
+    const dim3 grid((unsigned)ceil_div(n_seeds, 128)), block(128);
+    if (fixed_acc) {
+      const FixedHeat acc{fixed_acc};
+      if (probs)
+        hipLaunchKernelGGL(k_heat_bias<FixedHeat>, grid, block, 0, st, seeds, n_seeds, indptr,
+                           indices, probs, seeds_heat, num_picks, indptr_diff, acc);
+      else
+        hipLaunchKernelGGL(k_heat<FixedHeat>, grid, block, 0, st, seeds, n_seeds, indptr,
+                           indices, seeds_heat, num_picks, indptr_diff, acc);
+    } else {
+      const FloatHeat acc{frontier_heat};
+      if (probs)
+        hipLaunchKernelGGL(k_heat_bias<FloatHeat>, grid, block, 0, st, seeds, n_seeds, indptr,
+                           indices, probs, seeds_heat, num_picks, indptr_diff, acc);
+      else
+        hipLaunchKernelGGL(k_heat<FloatHeat>, grid, block, 0, st, seeds, n_seeds, indptr,
+                           indices, seeds_heat, num_picks, indptr_diff, acc);
+    }
+    DGS_LAUNCH_CHECK();
+  }
+  if (fixed_acc && num_nodes > 0) {
+    hipLaunchKernelGGL(k_heat_fixed_to_float, dim3((unsigned)ceil_div(num_nodes, 256)),
+                       dim3(256), 0, st, fixed_acc, num_nodes, frontier_heat);
+    DGS_LAUNCH_CHECK();
+  }
 }
 
 void cache_map_compact(const int64_t *tab, int64_t n, int64_t *key, int64_t *idx,

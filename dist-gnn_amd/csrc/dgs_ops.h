@@ -47,9 +47,12 @@ void ntab_assign(NodeEntry *ntab, const int64_t *nids, const int64_t *sub_indptr
 // location is a GPU; *d_count receives the count.  key/idx/devid may be null (count only).
 void cache_map_compact(const int64_t *tab, int64_t n, int64_t *key, int64_t *idx,
                        int64_t *devid, int64_t *d_count, hipStream_t st);
+// frontier heat (preprocess_heat.cu); fixed_acc != nullptr: deterministic fixed-point
+// accumulation in fixed_acc[num_nodes] (scratch), then written to frontier_heat as float
 void heat(const int64_t *seeds, int64_t n_seeds, const int64_t *indptr, const int64_t *indices,
           const float *probs, const float *seeds_heat, int64_t num_picks, int64_t indptr_diff,
-          float *frontier_heat, hipStream_t st);
+          float *frontier_heat, int64_t num_nodes, unsigned long long *fixed_acc,
+          hipStream_t st);
 
 // ---------------------------------------------------------------- scan (scan.hip)
 // Single-workgroup exclusive scan of n int64 values in place into out[0..n], out[n] = total.

@@ -52,6 +52,8 @@ _SIGS = {
     "dgs_extract_edge_data": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "dgs_compute_frontier_heat": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                           c_i64, c_vp, c_vp]),
+    "dgs_compute_frontier_heat_fixed": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                                c_i64, c_i64, c_vp, c_vp]),
     "dgs_p2p_server_create": (c_int, [c_vp, c_i64, c_i64, p_vp]),
     "dgs_p2p_server_device_ptr": (c_int, [c_vp, c_i64, p_vp, p_i64]),
     "dgs_p2p_server_destroy": (c_int, [c_vp]),

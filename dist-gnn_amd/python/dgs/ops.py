@@ -239,27 +239,31 @@ def _Test_ExtractEdgeData(nids, indptr, sub_indptr, edge_data):
 
 
 # ------------------------------------------------------------------ heat
-def _heat(seeds, indptr, indices, probs, seeds_heat, num_picks, indptr_diff):
+def _heat(seeds, indptr, indices, probs, seeds_heat, num_picks, indptr_diff, deterministic):
     s, ip, ix = as_i64(seeds, "seeds"), as_i64(indptr, "indptr"), as_i64(indices, "indices")
     if seeds_heat.dtype != torch.float32:
         raise RuntimeError("heat must be float32")
     fh = torch.zeros_like(seeds_heat)
     pr = probs.contiguous() if probs is not None else None
-    check(lib.dgs_compute_frontier_heat(ptr(s), s.numel(), ptr(ip), ptr(ix), ptr(pr),
-                                        ptr(seeds_heat), seeds_heat.numel(), int(num_picks),
-                                        int(indptr_diff), ptr(fh), stream_ptr(fh.device)))
+    fn = lib.dgs_compute_frontier_heat_fixed if deterministic else lib.dgs_compute_frontier_heat
+    check(fn(ptr(s), s.numel(), ptr(ip), ptr(ix), ptr(pr), ptr(seeds_heat), seeds_heat.numel(),
+             int(num_picks), int(indptr_diff), ptr(fh), stream_ptr(fh.device)))
     return fh
 
 
-def _CAPI_compute_frontier_heat(seeds, indptr, indices, seeds_heat, num_picks, indptr_diff):
-    """preprocess_heat.cu:35-56."""
-    return _heat(seeds, indptr, indices, None, seeds_heat, num_picks, indptr_diff)
+def _CAPI_compute_frontier_heat(seeds, indptr, indices, seeds_heat, num_picks, indptr_diff,
+                                deterministic=False):
+    """preprocess_heat.cu:35-56.  ADDITIVE deterministic=True: fixed-point accumulation
+    (order-independent; see dgs_compute_frontier_heat_fixed)."""
+    return _heat(seeds, indptr, indices, None, seeds_heat, num_picks, indptr_diff,
+                 deterministic)
 
 
 def _CAPI_compute_frontier_heat_with_bias(seeds, indptr, indices, probs, seeds_heat, num_picks,
-                                          indptr_diff):
+                                          indptr_diff, deterministic=False):
     """preprocess_heat.cu:100-121 (processes seeds.numel() - 1 seeds, as the reference)."""
-    return _heat(seeds, indptr, indices, probs, seeds_heat, num_picks, indptr_diff)
+    return _heat(seeds, indptr, indices, probs, seeds_heat, num_picks, indptr_diff,
+                 deterministic)
 
 
 PROFILE_GATHER, PROFILE_SAMPLE, PROFILE_SELECT = 1, 2, 4

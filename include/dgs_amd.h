@@ -109,6 +109,14 @@ int dgs_compute_frontier_heat(const int64_t *seeds, int64_t n_seeds, const int64
                               const int64_t *indices, const float *probs,
                               const float *seeds_heat, int64_t num_nodes, int64_t num_picks,
                               int64_t indptr_diff, float *frontier_heat, void *stream);
+/* ADDITIVE.  The same heat, accumulated deterministically: every message is rounded to a
+ * multiple of 2^-36 and summed in int64 (associative, so independent of atomic order), then
+ * converted to float.  Differs from the float-atomic form by at most 2^-37 per message. */
+int dgs_compute_frontier_heat_fixed(const int64_t *seeds, int64_t n_seeds,
+                                    const int64_t *indptr, const int64_t *indices,
+                                    const float *probs, const float *seeds_heat,
+                                    int64_t num_nodes, int64_t num_picks, int64_t indptr_diff,
+                                    float *frontier_heat, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * TensorP2PServer (src/cache/tensor_p2p_cache.{h,cc}; pybind.cc:41-45)
