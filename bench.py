@@ -140,9 +140,12 @@ def main():
 
     def step():
         seeds = next_seeds()
+        # the label gather depends only on the seeds: issued first, it runs while the host
+        # enters the sampler (the reference loop's order, node_classification.py:219-229, is
+        # sample -> features -> labels; the three are independent except features <- sample)
+        y = dgs.ops._CAPI_cuda_index_select(labels_dev, seeds)
         blocks = sampler._CAPI_sample_node_classifiction(seeds, fan_out, False)
         x = server._CAPI_get_feature(blocks[-1][1])
-        y = dgs.ops._CAPI_cuda_index_select(labels_dev, seeds)
         return sum(b[2].numel() for b in blocks), x.shape[0], x, y
 
     for _ in range(args.warmup):
