@@ -84,10 +84,12 @@ struct HopScratch {
 //   writes rowpos[e] (index of the seed row of edge e) and col[e] (neighbour nid),
 //   d_nnz receives nnz (device).  Capacities: S.v * k.
 // When `table.key` is set, every seed i and sampled neighbour (position S + e) is inserted
-// into the relabel table by the kernels that produce them.
+// into the relabel table by the kernels that produce them.  `tail` (the previous hop's
+// deferred relabel pass, on the other table) runs in the same launch as this hop's prep.
 void sample_hop(const RowSrc &src, const int64_t *seeds, Count S, int64_t k, bool replace,
                 bool bias, uint64_t launch_seed, int64_t *rowpos, int64_t *col, int64_t *d_nnz,
-                const Table &table, HopScratch &ws, hipStream_t st);
+                const Table &table, HopScratch &ws, hipStream_t st,
+                const RelabelTail *tail = nullptr);
 
 // Clean relabel table with capacity for n_ub insertions (marks the scratch dirty until the
 // hop's relabel pass has returned the touched slots to empty).
@@ -105,7 +107,10 @@ Table direct_table(DevBuf &val, DevBuf &lab, int64_t num_nodes, bool *dirty, hip
 void relabel_hop(const int64_t *seeds, Count S, const int64_t *col, const int64_t *d_nnz,
                  int64_t nnz_cap, bool seeds_unique, const Table &table, int64_t *unique,
                  int64_t *out_row, int64_t *out_col, int64_t *d_nunique, HopScratch &ws,
-                 hipStream_t st, const HostSizes &pub = HostSizes{});
+                 hipStream_t st, const HostSizes &pub = HostSizes{},
+                 RelabelTail *defer = nullptr);
+// launches a deferred relabel tail on its own
+void launch_relabel_tail(const RelabelTail &tail, hipStream_t st);
 
 // Generic relabel (TensorRelabelCUDA): mapping[nm], req[nr] -> unique, relabeled req (-1 if
 // absent), d_nunique.

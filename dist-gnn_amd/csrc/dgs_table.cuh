@@ -24,7 +24,35 @@ struct Table {
 };
 
 
+// The last pass of a hop's relabel (direct layout): out_col[e] = lab[col[e]] in place,
+// out_row[e] = lab[seeds[r]] when the seeds may repeat (else label(r) == r), then every touched
+// node's val returns to empty.  Kept as a descriptor so the sampler can run it in the same
+// launch as the next hop's prep (which uses the other table).
+struct RelabelTail {
+  const int64_t *seeds;
+  Count Sc;
+  const int64_t *d_nb;
+  Table t;
+  int remap_rows;
+  int64_t *out_row;
+  int64_t *out_col;
+  int64_t nblk;  // 256-thread blocks covering max(S, nnz) (upper bounds)
+};
+
 #ifdef __HIPCC__
+__device__ __forceinline__ void relabel_tail_block(const RelabelTail &r, int64_t blk) {
+  const int64_t na = r.Sc.get();
+  const int64_t nb = *r.d_nb;
+  const int64_t e = blk * 256 + threadIdx.x;
+  if (e < nb) {
+    const int64_t v = r.out_col[e];
+    r.out_col[e] = r.t.lab[v];
+    if (r.remap_rows) r.out_row[e] = r.t.lab[r.seeds[r.out_row[e]]];
+    r.t.val[v] = kTableNoPos;
+  }
+  if (e < na) r.t.val[r.seeds[e]] = kTableNoPos;
+}
+
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
   k ^= k >> 33;
   k *= 0xff51afd7ed558ccdULL;

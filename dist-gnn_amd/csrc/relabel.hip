@@ -200,22 +200,8 @@ __global__ __launch_bounds__(kThreads) void k_dscatter(const int64_t *a, Count n
   }
 }
 
-// out_col[e] = lab[col[e]] in place; out_row[e] = lab[seeds[r]] when the seeds may repeat
-// (else label(r) == r, see k_relabel_hop); then every touched node's val returns to empty.
-__global__ __launch_bounds__(kThreads) void k_drelabel_hop(const int64_t *seeds, Count nac,
-                                                           const int64_t *d_nb, Table t,
-                                                           int remap_rows, int64_t *out_row,
-                                                           int64_t *out_col) {
-  const int64_t na = nac.get();
-  const int64_t nb = *d_nb;
-  const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (e < nb) {
-    const int64_t v = out_col[e];
-    out_col[e] = t.lab[v];
-    if (remap_rows) out_row[e] = t.lab[seeds[out_row[e]]];
-    t.val[v] = kNoPos;
-  }
-  if (e < na) t.val[seeds[e]] = kNoPos;
+__global__ __launch_bounds__(kThreads) void k_drelabel_hop(RelabelTail r) {
+  relabel_tail_block(r, blockIdx.x);
 }
 
 __global__ void k_fill_i32(int32_t *p, int64_t n, int32_t v) {
@@ -272,6 +258,11 @@ Table relabel_table(HopScratch &ws, int64_t n_ub, hipStream_t st) {
                ws.slot_of.as<uint32_t>(), cap - 1, false};
 }
 
+void launch_relabel_tail(const RelabelTail &tail, hipStream_t st) {
+  hipLaunchKernelGGL(k_drelabel_hop, dim3((unsigned)tail.nblk), dim3(kThreads), 0, st, tail);
+  DGS_LAUNCH_CHECK();
+}
+
 Table direct_table(DevBuf &val, DevBuf &lab, int64_t num_nodes, bool *dirty, hipStream_t st) {
   const int64_t n = num_nodes > 0 ? num_nodes : 1;
   const bool fresh = val.ensure(sizeof(int32_t) * (size_t)n);
@@ -291,7 +282,7 @@ Table direct_table(DevBuf &val, DevBuf &lab, int64_t num_nodes, bool *dirty, hip
 void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64_t *d_nnz,
                  int64_t nnz_cap, bool seeds_unique, const Table &t, int64_t *unique,
                  int64_t *out_row, int64_t *out_col, int64_t *d_nunique, HopScratch &ws,
-                 hipStream_t st, const HostSizes &pub) {
+                 hipStream_t st, const HostSizes &pub, RelabelTail *defer) {
   const int64_t n_ub = Sc.v + nnz_cap;
   const int64_t nblk = ceil_div(n_ub > 0 ? n_ub : 1, kThreads);
   ws.misc.ensure(sizeof(int64_t) * (size_t)(2 * nblk + 2));
@@ -306,9 +297,13 @@ void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64
     hipLaunchKernelGGL(k_dscatter, dim3((unsigned)ntiles), dim3(kThreads), 0, st, seeds, Sc,
                        col, d_nnz, t, (const int64_t *)tcnt, unique, d_nunique, pub);
     DGS_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_drelabel_hop, dim3((unsigned)nblk), dim3(kThreads), 0, st, seeds, Sc,
-                       d_nnz, t, (int)!seeds_unique, out_row, out_col);
-    DGS_LAUNCH_CHECK();
+    const RelabelTail tail{seeds, Sc, d_nnz, t, (int)!seeds_unique, out_row, out_col, nblk};
+    if (defer) {
+      *defer = tail;  // the caller launches it with the next hop's prep
+    } else {
+      hipLaunchKernelGGL(k_drelabel_hop, dim3((unsigned)nblk), dim3(kThreads), 0, st, tail);
+      DGS_LAUNCH_CHECK();
+    }
     return;
   }
   hipLaunchKernelGGL(k_flag_count, dim3((unsigned)nblk), dim3(kThreads), 0, st, Sc, d_nnz,

@@ -93,59 +93,83 @@ struct HubView {
 // ------------------------------------------------------------------------------------
 // Prep: per-row lookup (one 16-byte node-table load), per-row in-tile output prefix, tile
 // sums, hub detection (+ hub slot initialisation, slot s = s: rowwise_sampling.cu:80-82).
-__global__ __launch_bounds__(kTileRows) void k_prep(RowSrc src, const int64_t *__restrict__ seeds,
-                                                    Count Sc, int64_t k, int replace,
-                                                    int use_hubs, int bias_replace,
-                                                    RowInfo *__restrict__ rowinfo,
-                                                    int32_t *__restrict__ tpre,
-                                                    int32_t *__restrict__ tpre2,
-                                                    int64_t *__restrict__ bsum,
-                                                    int64_t *__restrict__ tsum, HubView hub,
-                                                    int32_t *__restrict__ hubslot, Table table,
-                                                    int64_t *next_hub_count) {
+struct PrepArgs {
+  RowSrc src;
+  const int64_t *seeds;
+  Count Sc;
+  int64_t k;
+  int replace;
+  int use_hubs;  // 0 none, 1 uniform hubs, 2 biased hubs
+  int bias_replace;
+  RowInfo *rowinfo;
+  int32_t *tpre;
+  int32_t *tpre2;
+  int64_t *bsum;
+  int64_t *tsum;
+  HubView hub;
+  int32_t *hubslot;
+  Table table;
+  int64_t *next_hub_count;
+};
+
+__device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
   __shared__ int64_t lds[kTileRows / 64];
-  const int64_t S = Sc.get();
+  const int64_t S = a.Sc.get();
+  const int64_t k = a.k;
   // the next hop's counter was last used two hops ago: reset it here (no memset launch)
-  if (blockIdx.x == 0 && threadIdx.x == 0) *next_hub_count = 0;
-  if ((int64_t)blockIdx.x * kTileRows >= S) return;  // whole workgroup past the live rows
-  const int64_t i = (int64_t)blockIdx.x * kTileRows + threadIdx.x;
+  if (blk == 0 && threadIdx.x == 0) *a.next_hub_count = 0;
+  if (blk * kTileRows >= S) return;  // whole workgroup past the live rows
+  const int64_t i = blk * kTileRows + threadIdx.x;
   int64_t cnt = 0, tdeg = 0;
   if (i < S) {
-    const int64_t v = seeds[i];
-    const RowInfo ri = lookup_row(src, v);
-    rowinfo[i] = ri;
-    table_record(table, v, i);
+    const int64_t v = a.seeds[i];
+    const RowInfo ri = lookup_row(a.src, v);
+    a.rowinfo[i] = ri;
+    table_record(a.table, v, i);
     const int64_t deg = ri_deg(ri);
-    cnt = row_count(deg, k, replace);
+    cnt = row_count(deg, k, a.replace);
     tdeg = deg;
-    if (use_hubs) {
+    if (a.use_hubs) {
       int64_t h = -1;
       // 1: uniform hubs (reservoir tail > kHubT, 512-edge chunks); 2: biased hubs (degree >
       // kBiasHubT, kBiasChunk-edge chunks)
-      const bool is_hub = use_hubs == 1 ? deg - k > kHubT : deg > kBiasHubT;
+      const bool is_hub = a.use_hubs == 1 ? deg - k > kHubT : deg > kBiasHubT;
       if (is_hub) {
-        const uint64_t nch = use_hubs == 1 ? (uint64_t)(deg - k + 511) / 512
-                                           : (uint64_t)(deg + kBiasChunk - 1) / kBiasChunk;
-        const uint64_t old = atomicAdd((unsigned long long *)hub.count,
+        const uint64_t nch = a.use_hubs == 1 ? (uint64_t)(deg - k + 511) / 512
+                                             : (uint64_t)(deg + kBiasChunk - 1) / kBiasChunk;
+        const uint64_t old = atomicAdd((unsigned long long *)a.hub.count,
                                        (unsigned long long)((uint64_t(1) << kHubShift) | nch));
         h = (int64_t)(old >> kHubShift);
-        hub.row[h] = i;
-        hub.cptr[h] = (int64_t)(old & kHubChunkMask);
-        if (use_hubs == 1)
-          for (int64_t s2 = 0; s2 < k; ++s2) hubslot[h * k + s2] = (int32_t)s2;
+        a.hub.row[h] = i;
+        a.hub.cptr[h] = (int64_t)(old & kHubChunkMask);
+        if (a.use_hubs == 1)
+          for (int64_t s2 = 0; s2 < k; ++s2) a.hubslot[h * k + s2] = (int32_t)s2;
       }
-      hub.hubid[i] = h;
+      a.hub.hubid[i] = h;
     }
   }
   int64_t tot;
   const int64_t ex = block_exclusive_scan<kTileRows>(cnt, &tot, lds);
-  if (i < S) tpre[i] = (int32_t)ex;
-  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
-  if (bias_replace) {
+  if (i < S) a.tpre[i] = (int32_t)ex;
+  if (threadIdx.x == 0) a.bsum[blk] = tot;
+  if (a.bias_replace) {
     const int64_t ex2 = block_exclusive_scan<kTileRows>(tdeg, &tot, lds);
-    if (i < S) tpre2[i] = (int32_t)ex2;
-    if (threadIdx.x == 0) tsum[blockIdx.x] = tot;
+    if (i < S) a.tpre2[i] = (int32_t)ex2;
+    if (threadIdx.x == 0) a.tsum[blk] = tot;
   }
+}
+
+// Prep: per-row lookup (one 16-byte node-table load), in-tile output prefix, tile sums, hub
+// registration, relabel insert of the seeds.
+__global__ __launch_bounds__(kTileRows) void k_prep(PrepArgs a) { prep_block(a, blockIdx.x); }
+
+// The previous hop's relabel pass (blocks [0, tail.nblk), on the other relabel table) and this
+// hop's prep in one launch: both only need the previous hop's unique frontier.
+__global__ __launch_bounds__(kTileRows) void k_prep_tail(PrepArgs a, RelabelTail tail) {
+  if ((int64_t)blockIdx.x < tail.nblk)
+    relabel_tail_block(tail, blockIdx.x);
+  else
+    prep_block(a, (int64_t)blockIdx.x - tail.nblk);
 }
 
 // Single workgroup: exclusive scan of tile sums (-> boff[0..nb], boff[nb] = nnz; the same for
@@ -867,7 +891,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
 // ------------------------------------------------------------------------------------
 void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bool replace,
                 bool bias, uint64_t launch_seed, int64_t *rowpos, int64_t *col, int64_t *d_nnz,
-                const Table &table, HopScratch &ws, hipStream_t st) {
+                const Table &table, HopScratch &ws, hipStream_t st, const RelabelTail *tail) {
   DGS_CHECK(k >= 0, "num_picks must be non-negative");
   const int64_t S = Sc.v;  // exact when Sc.p == nullptr, else an upper bound
   DGS_CHECK(S < (int64_t(1) << 31), "too many seeds in one hop");
@@ -881,6 +905,7 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   int64_t *tboff = boff + nb + 1;
   RowInfo *rowinfo = ws.rowinfo.as<RowInfo>();
   if (S == 0) {
+    if (tail) launch_relabel_tail(*tail, st);
     DGS_HIP(hipMemsetAsync(d_nnz, 0, sizeof(int64_t), st));
     return;
   }
@@ -899,10 +924,14 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   int32_t *tpre = ws.tpre.as<int32_t>();
   int32_t *tpre2 = tpre + S;
   if (use_hubs) ws.hubslot.ensure(sizeof(int32_t) * (size_t)(S * k));
-  hipLaunchKernelGGL(k_prep, dim3((unsigned)nb), dim3(kTileRows), 0, st, src, seeds, Sc, k,
-                     (int)replace, use_hubs ? 1 : (bias_hubs ? 2 : 0), (int)bias_replace, rowinfo,
-                     tpre, tpre2, bsum,
-                     tsum, hub, ws.hubslot.as<int32_t>(), table, next_count);
+  const PrepArgs pa{src, seeds, Sc, k, (int)replace, use_hubs ? 1 : (bias_hubs ? 2 : 0),
+                    (int)bias_replace, rowinfo, tpre, tpre2, bsum, tsum, hub,
+                    ws.hubslot.as<int32_t>(), table, next_count};
+  if (tail)
+    hipLaunchKernelGGL(k_prep_tail, dim3((unsigned)(tail->nblk + nb)), dim3(kTileRows), 0, st, pa,
+                       *tail);
+  else
+    hipLaunchKernelGGL(k_prep, dim3((unsigned)nb), dim3(kTileRows), 0, st, pa);
   DGS_LAUNCH_CHECK();
   if (k == 0) {  // seeds still enter the relabel table (frontier = unique(seeds))
     DGS_HIP(hipMemsetAsync(d_nnz, 0, sizeof(int64_t), st));

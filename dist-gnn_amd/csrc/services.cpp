@@ -205,6 +205,11 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
   const int64_t *cur = seeds;
   Count S{n_seeds, nullptr};
   profile_begin(st, 1);
+  // Relabel tables alternate between hops (hop h uses table h & 1): the last pass of hop h's
+  // relabel, which empties table h & 1, runs in the same launch as hop h+1's prep, which fills
+  // the other one.
+  RelabelTail tail{};
+  bool have_tail = false;
   for (int h = 0; h < L; ++h) {
     const int64_t k = fan_out[L - 1 - h];
     DGS_CHECK(k >= 0, "fan_out entries must be non-negative");
@@ -212,15 +217,20 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
     const int64_t nnz_cap = ecap[h];
     int64_t *d_nnz = dsz + 3 * h + 2;
     int64_t *d_uniq = dsz + 3 * h + 1;
-    const Table t = direct_table(dval_, dlab_, num_nodes_, &dtab_dirty_, st);
-    dtab_dirty_ = true;
+    const int tb = h & 1;
+    const Table t = direct_table(dval_[tb], dlab_[tb], num_nodes_, &dtab_dirty_[tb], st);
+    dtab_dirty_[tb] = true;
     // rows[h] receives each edge's seed row r from the sampler and is relabelled in place
-    sample_hop(src_, cur, S, k, replace, bias_, seed, rows[h], cols[h], d_nnz, t, ws_, st);
+    sample_hop(src_, cur, S, k, replace, bias_, seed, rows[h], cols[h], d_nnz, t, ws_, st,
+               have_tail ? &tail : nullptr);
+    if (have_tail) dtab_dirty_[tb ^ 1] = false;  // the previous hop's clean-up is enqueued
     // the last hop's scatter publishes every size to pinned host memory (no copy, no sync)
-    const HostSizes pub = h == L - 1 ? HostSizes{dsz, 3 * L, sizes_host_dev_, seq} : HostSizes{};
+    const bool last = h == L - 1;
+    const HostSizes pub = last ? HostSizes{dsz, 3 * L, sizes_host_dev_, seq} : HostSizes{};
     relabel_hop(cur, S, cols[h], d_nnz, nnz_cap, /*seeds_unique=*/h > 0, t, frontiers[h],
-                rows[h], cols[h], d_uniq, ws_, st, pub);
-    dtab_dirty_ = false;  // the relabel pass just enqueued empties what this hop touched
+                rows[h], cols[h], d_uniq, ws_, st, pub, last ? nullptr : &tail);
+    have_tail = !last;
+    if (last) dtab_dirty_[tb] = false;
     cur = frontiers[h];
     S = Count{fcap[h], d_uniq};
   }

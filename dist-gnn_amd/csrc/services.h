@@ -82,8 +82,8 @@ class Sampler {
   DevBuf ntab_;
   RowSrc src_{};
   HopScratch ws_;
-  DevBuf dval_, dlab_;  // direct relabel table over node ids (first position, label)
-  bool dtab_dirty_ = false;
+  DevBuf dval_[2], dlab_[2];  // direct relabel tables over node ids (first position, label),
+  bool dtab_dirty_[2] = {false, false};  // used by alternate hops
   DevBuf sizes_;
   HostPinned sizes_host_;  // [0] publication sequence, [1..3L] per-hop sizes
   int64_t *sizes_host_dev_ = nullptr;
