@@ -325,3 +325,25 @@ def test_rmat_scale16_sampler_bit_exact(dgs):
         assert np.array_equal(gf.cpu().numpy(), ef)
         assert np.array_equal(gr.cpu().numpy(), er)
         assert np.array_equal(gc.cpu().numpy(), ec)
+
+
+@pytest.mark.parametrize("fan_out,replace", [([15, 10, 5], False), ([25, 10], False),
+                                             ([8, 4, 2], True)])
+def test_rmat_biased_multihop_bit_exact(dgs, fan_out, replace):
+    """Degree-weighted biased sampling over a power-law graph: hub rows split across
+    half-waves (chain RNG offsets, batched top-k merges) and the row kernel, 2-3 hops."""
+    from DistGNN.dataloading.synthetic import degree_probs, rmat_csc_numpy
+    indptr, indices = rmat_csc_numpy(14, 16, seed=7)
+    probs = degree_probs(indptr, indices)
+    n = indptr.size - 1
+    sampler = dgs.classes.P2PCacheSampler(torch.from_numpy(indptr), torch.from_numpy(indices),
+                                          torch.from_numpy(probs), torch.arange(n), 0)
+    seeds = np.random.default_rng(5).permutation(n)[:700]
+    dgs.ops._CAPI_set_random_seed(123)
+    got = sampler._CAPI_sample_node_classifiction(_cuda(seeds), fan_out, replace)
+    exp = O.node_classification_sample(seeds, indptr, indices, fan_out, replace,
+                                       O.launch_seeds(123, len(fan_out)), probs=probs)
+    for (gs, gf, gr, gc), (es, ef, er, ec) in zip(got, exp):
+        assert np.array_equal(gf.cpu().numpy(), ef)
+        assert np.array_equal(gr.cpu().numpy(), er)
+        assert np.array_equal(gc.cpu().numpy(), ec)
