@@ -850,17 +850,23 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
   for (int64_t h = blockIdx.x; h < H; h += gridDim.x) {
     const int64_t wf = a.wfirst[h], wl = a.wlast[h];
     HalfTopK top;
-    for (int64_t w = wf + g; w <= wl; w += 8) {
-      if (bias_worker_c0(total, w, nw) == bias_worker_c0(total, w + 1, nw)) continue;  // empty
+    // k <= 16: two workers' lists per batch (lanes 0-15 and 16-31), else one
+    const int per = k <= 16 ? 2 : 1;
+    const int part = per == 2 ? (l >> 4) : 0;
+    const int e = per == 2 ? (l & 15) : l;
+    for (int64_t w0 = wf + (int64_t)per * g; w0 <= wl; w0 += 8 * per) {
+      const int64_t w = w0 + part;
+      bool have = w <= wl && bias_worker_c0(total, w, nw) != bias_worker_c0(total, w + 1, nw);
       const int64_t slot = w + h;
-      const int n = a.ccnt[slot];
+      const int n = have ? a.ccnt[slot] : 0;
+      const bool valid = e < n;
       float key_i = -__builtin_inff();
       int64_t i = INT64_MAX;
-      if (l < n) {
-        key_i = a.ckey[slot * k + l];
-        i = a.cidx[slot * k + l];
+      if (valid) {
+        key_i = a.ckey[slot * k + e];
+        i = a.cidx[slot * k + e];
       }
-      top.push(key_i, i, l < n, k, l);
+      top.push(key_i, i, valid, k, l);
     }
     s_key[g][l] = top.bk;
     s_idx[g][l] = top.bi;
