@@ -157,6 +157,7 @@ int dgs_sample_neighbors(const int64_t *seeds, int64_t Sn, const int64_t *indptr
     src.indices = dev_ptr(indices, "indices");
     src.indices_base.p[0] = src.indices;
     src.probs.p[0] = dev_ptr(probs, "probs");
+    src.num_nodes = INT64_MAX;  // no node count at this boundary (reference: unchecked)
     seeds = dev_ptr(seeds, "seeds");
     HopScratch &ws = op_scratch();
     int64_t *tmp = nullptr;  // [0] = nnz, then rowpos[S*k]

@@ -69,6 +69,11 @@ struct RowSrc {
   const int64_t *indices;  // plain-CSR neighbour ids
   PtrTable indices_base;   // per-location neighbour-id arrays (to locate probs)
   PtrTable probs;          // per-location probabilities (biased) or all null
+  // Seed validation (sampler only): a seed outside [0, num_nodes) is sampled as a degree-0
+  // row, kept out of the relabel table, and reported by storing bad_tag to *bad.
+  int64_t num_nodes;
+  int64_t *bad;
+  int64_t bad_tag;
 };
 
 struct HopScratch {

@@ -21,6 +21,7 @@ struct Table {
   uint32_t *slot_of;  // hashed layout: slot of every inserted position
   uint64_t mask;  // hashed layout: capacity - 1
   bool direct;
+  int64_t n;      // direct layout: number of node ids (ids outside [0, n) are never recorded)
 };
 
 
@@ -50,7 +51,10 @@ __device__ __forceinline__ void relabel_tail_block(const RelabelTail &r, int64_t
     if (r.remap_rows) r.out_row[e] = r.t.lab[r.seeds[r.out_row[e]]];
     r.t.val[v] = kTableNoPos;
   }
-  if (e < na) r.t.val[r.seeds[e]] = kTableNoPos;
+  if (e < na) {
+    const int64_t s = r.seeds[e];
+    if ((uint64_t)s < (uint64_t)r.t.n) r.t.val[s] = kTableNoPos;
+  }
 }
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {

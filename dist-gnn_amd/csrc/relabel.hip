@@ -140,7 +140,8 @@ __device__ __forceinline__ int64_t first_flags(const int64_t *a, int64_t na, con
     x[j] = *src;
   }
 #pragma unroll
-  for (int j = 0; j < kCompactItems; ++j) pv[j] = t.val[x[j]];
+  for (int j = 0; j < kCompactItems; ++j)
+    pv[j] = (uint64_t)x[j] < (uint64_t)t.n ? t.val[x[j]] : kNoPos;
   int64_t cnt = 0;
 #pragma unroll
   for (int j = 0; j < kCompactItems; ++j) {
@@ -273,7 +274,7 @@ Table direct_table(DevBuf &val, DevBuf &lab, int64_t num_nodes, bool *dirty, hip
     DGS_LAUNCH_CHECK();
     *dirty = false;
   }
-  return Table{nullptr, val.as<int32_t>(), lab.as<int32_t>(), nullptr, 0, true};
+  return Table{nullptr, val.as<int32_t>(), lab.as<int32_t>(), nullptr, 0, true, num_nodes};
 }
 
 // The hop's seeds and sampled neighbours were already inserted by the sampling kernels

@@ -123,9 +123,14 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
   int64_t cnt = 0, tdeg = 0;
   if (i < S) {
     const int64_t v = a.seeds[i];
-    const RowInfo ri = lookup_row(a.src, v);
+    const bool ok = (uint64_t)v < (uint64_t)a.src.num_nodes;
+    const RowInfo ri = ok ? lookup_row(a.src, v) : RowInfo{nullptr, 0};
     a.rowinfo[i] = ri;
-    table_record(a.table, v, i);
+    if (ok) {
+      table_record(a.table, v, i);
+    } else if (a.src.bad) {
+      *a.src.bad = a.src.bad_tag;
+    }
     const int64_t deg = ri_deg(ri);
     cnt = row_count(deg, k, a.replace);
     tdeg = deg;

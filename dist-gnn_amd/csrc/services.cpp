@@ -153,6 +153,7 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
   }
   src_.indices_base.p[kLocHost] = h_indices_.dev;
   src_.probs.p[kLocHost] = bias_ ? h_probs_.dev : nullptr;
+  src_.num_nodes = num_nodes;
 }
 
 Sampler::~Sampler() {
@@ -186,7 +187,10 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
                      bool replace, int64_t *const *frontiers, int64_t *const *rows,
                      int64_t *const *cols, int64_t *sizes, hipStream_t st) {
   if (L <= 0) return;
-  sizes_.ensure(sizeof(int64_t) * (size_t)(3 * L + 1));
+  // device sizes: 3 per hop, then the bad-seed word (holds the seq of the last call that saw
+  // a seed outside [0, num_nodes); zeroed at allocation, never reset)
+  if (sizes_.ensure(sizeof(int64_t) * (size_t)(3 * L + 1)))
+    DGS_HIP(hipMemsetAsync(sizes_.p, 0, sizes_.bytes, st));
   if (sizes_host_.bytes < sizeof(int64_t) * (size_t)(3 * L + 2)) {
     sizes_host_.flags = hipHostMallocCoherent | hipHostMallocMapped;
     sizes_host_.ensure(sizeof(int64_t) * (size_t)(3 * L + 2));
@@ -200,6 +204,9 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
   if (seq_ > 0 && st != last_stream_) DGS_HIP(hipStreamSynchronize(last_stream_));
   last_stream_ = st;
   const uint64_t seq = ++seq_;
+  RowSrc src = src_;
+  src.bad = dsz + 3 * L;
+  src.bad_tag = (int64_t)seq;
   std::vector<int64_t> fcap(L), ecap(L);
   bounds(n_seeds, fan_out, L, fcap.data(), ecap.data());
   const int64_t *cur = seeds;
@@ -221,12 +228,12 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
     const Table t = direct_table(dval_[tb], dlab_[tb], num_nodes_, &dtab_dirty_[tb], st);
     dtab_dirty_[tb] = true;
     // rows[h] receives each edge's seed row r from the sampler and is relabelled in place
-    sample_hop(src_, cur, S, k, replace, bias_, seed, rows[h], cols[h], d_nnz, t, ws_, st,
+    sample_hop(src, cur, S, k, replace, bias_, seed, rows[h], cols[h], d_nnz, t, ws_, st,
                have_tail ? &tail : nullptr);
     if (have_tail) dtab_dirty_[tb ^ 1] = false;  // the previous hop's clean-up is enqueued
     // the last hop's scatter publishes every size to pinned host memory (no copy, no sync)
     const bool last = h == L - 1;
-    const HostSizes pub = last ? HostSizes{dsz, 3 * L, sizes_host_dev_, seq} : HostSizes{};
+    const HostSizes pub = last ? HostSizes{dsz, 3 * L + 1, sizes_host_dev_, seq} : HostSizes{};
     relabel_hop(cur, S, cols[h], d_nnz, nnz_cap, /*seeds_unique=*/h > 0, t, frontiers[h],
                 rows[h], cols[h], d_uniq, ws_, st, pub, last ? nullptr : &tail);
     have_tail = !last;
@@ -251,6 +258,10 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
     }
     __builtin_ia32_pause();
   }
+  // A call with a bad seed fails after it has run (its rows were sampled as empty; the
+  // reference reads out of bounds instead).
+  DGS_CHECK(hsz[1 + 3 * L] != (int64_t)seq,
+            "sample: a seed is outside [0, num_nodes)");
   int64_t s = n_seeds;
   for (int h = 0; h < L; ++h) {
     sizes[3 * h + 0] = s;

@@ -225,6 +225,29 @@ def test_p2p_cache_sampler_matches_oracle(dgs, cache, replace, bias):
         assert np.array_equal(gc.cpu().numpy(), ec)
 
 
+@pytest.mark.parametrize("bad", [-1, "n", 1 << 40])
+def test_sampler_rejects_out_of_range_seed(dgs, bad):
+    # The reference reads out of bounds here; this path samples the bad row as empty, keeps it
+    # out of the relabel table and raises after the call.  The tables must stay clean: the next
+    # call is still bit-exact.
+    indptr, indices, probs = _hub_graph(11)
+    n = indptr.size - 1
+    sampler = dgs.classes.P2PCacheSampler(torch.from_numpy(indptr), torch.from_numpy(indices),
+                                          torch.Tensor(), torch.arange(0, n, 2), 0)
+    seeds = np.random.default_rng(5).permutation(n)[:64]
+    badseeds = seeds.copy()
+    badseeds[7] = n if bad == "n" else bad
+    with pytest.raises(RuntimeError, match="outside"):
+        sampler._CAPI_sample_node_classifiction(_cuda(badseeds), [15, 10, 5], False)
+    dgs.ops._CAPI_set_random_seed(99)
+    got = sampler._CAPI_sample_node_classifiction(_cuda(seeds), [15, 10, 5], False)
+    exp = O.node_classification_sample(seeds, indptr, indices, [15, 10, 5], False,
+                                       O.launch_seeds(99, 3))
+    for g, e in zip(got, exp):
+        for a, b in zip(g, e):
+            assert np.array_equal(a.cpu().numpy(), b)
+
+
 def test_sampler_getters(dgs):
     with open(os.path.join(GOLD, "reference_kats.json")) as f:
         g = json.load(f)["toy_graph"]
