@@ -15,6 +15,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--scale 
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -48,6 +49,9 @@ def parse():
                    help="cache node v on GPU v %% N (P2P over xGMI) instead of replicating")
     p.add_argument("--bias", action="store_true",
                    help="biased (degree-weighted) sampler: probs[e] = 1 + indeg(indices[e])")
+    p.add_argument("--cache-frac", type=float, default=1.0,
+                   help="cache only the ceil(f*N) highest in-degree nodes in HBM; every other "
+                        "row is read zero-copy from pinned host memory (SURVEY 8(f) rank 2)")
     p.add_argument("--comm", choices=["gloo", "rccl"], default="gloo",
                    help="transport of the library's setup collectives in --shard mode")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
@@ -99,6 +103,12 @@ def main():
     feats_d = torch.randn(N, args.dim, generator=gen, device=dev)
     labels_d = torch.randint(0, 47, (N,), generator=gen, device=dev)
     probs = torch.Tensor()
+    hot = None
+    if args.cache_frac < 1.0:  # hot set: highest in-degree first (ties by id), kept on host
+        n_hot = max(1, int(math.ceil(args.cache_frac * N)))
+        indeg = torch.bincount(indices_d, minlength=indptr_d.numel() - 1)
+        hot = torch.sort(indeg, descending=True, stable=True).indices[:n_hot].cpu()
+        del indeg
     if args.bias:  # degree-weighted, probs[e] = float32(1 + indeg(indices[e]))
         indeg = torch.bincount(indices_d, minlength=indptr_d.numel() - 1)
         probs = (1 + indeg[indices_d]).to(torch.float32).cpu()
@@ -114,10 +124,15 @@ def main():
     log(f"[bench] graph N={N} E={E} d={args.dim} built in {time.time() - t0:.1f}s")
 
     # ---------------- services: whole graph + all features in HBM (configs[1])
-    if args.shard and world > 1:
+    if hot is not None:
+        cache = hot[rank::world] if args.shard and world > 1 else hot
+    elif args.shard and world > 1:
         cache = torch.arange(rank, N, world)
     else:
         cache = torch.arange(N)
+    # which nodes any GPU holds (the rest are host rows), for the host-row share reported below
+    cached_mask = torch.zeros(N, dtype=torch.bool, device=dev)
+    cached_mask[(hot if hot is not None else torch.arange(N)).to(dev)] = True
     t0 = time.time()
     sampler = dgs.classes.P2PCacheSampler(indptr, indices, probs, cache, local_rank)
     server = dgs.classes.P2PCacheFeatureServer(feats, cache, local_rank)
@@ -146,7 +161,7 @@ def main():
         y = dgs.ops._CAPI_cuda_index_select(labels_dev, seeds)
         blocks = sampler._CAPI_sample_node_classifiction(seeds, fan_out, False)
         x = server._CAPI_get_feature(blocks[-1][1])
-        return sum(b[2].numel() for b in blocks), x.shape[0], x, y
+        return sum(b[2].numel() for b in blocks), x.shape[0], x, y, blocks[-1][1]
 
     for _ in range(args.warmup):
         step()
@@ -160,7 +175,7 @@ def main():
     edges = rows = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        e, r, _, _ = step()
+        e, r, _, _, _ = step()
         edges += e
         rows += r
     torch.cuda.synchronize()
@@ -171,8 +186,11 @@ def main():
     prof = dgs.ops.profile_read()
     # informational, outside the timed region: GPU span of the sample call and label select
     dgs.ops.profile_enable(dgs.ops.PROFILE_SAMPLE | dgs.ops.PROFILE_SELECT)
+    host_rows = 0.0
     for _ in range(min(args.steps, 20)):
-        step()
+        nids = step()[4]
+        host_rows += float((~cached_mask[nids]).sum()) / max(nids.numel(), 1)
+    host_rows /= min(args.steps, 20)
     torch.cuda.synchronize()
     side = dgs.ops.profile_read()
     dgs.ops.profile_enable(False)
@@ -219,11 +237,19 @@ def main():
                          f"{'biased (degree-weighted)' if args.bias else 'uniform'} sampler "
                          f"fan-out {fan_out} without replacement, B={args.batch} "
                          f"seeds/step/GPU, + full-feature gather d={args.dim} f32 + label gather; "
-                         + ("graph sharded v%N over GPUs (P2P)" if args.shard and world > 1
+                         + (f"HBM cache of the {args.cache_frac:.0%} highest in-degree nodes "
+                            f"({'sharded' if args.shard and world > 1 else 'replicated'}), "
+                            "other rows zero-copy from pinned host" if hot is not None else
+                            "graph sharded v%N over GPUs (P2P)" if args.shard and world > 1
                             else "whole graph + features in HBM on every GPU")),
             "fan_out": fan_out, "batch_per_gpu": args.batch, "num_nodes": N, "num_edges": E,
             "feat_dim": args.dim, "parallelism": f"dp{world} (seed-parallel)",
+            "cache_frac": args.cache_frac,
         },
+        "host_row_share": host_rows,
+        # host rows cross PCIe Gen5 x16 (63 GB/s spec): their read rate during the gather
+        "gather_host_read_GBps": (host_rows * rows * row_bytes / (prof["gather_ms"] * 1e-3) / 1e9
+                                  if prof["gather_ms"] > 0 else 0.0),
         "gather_GBps": achieved,
         "gather_GBps_wall": gbytes_all / elapsed / 1e9,
         "sampled_edges_per_step": edges_all / args.steps,
