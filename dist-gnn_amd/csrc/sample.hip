@@ -148,7 +148,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
         a.hub.row[h] = i;
         a.hub.cptr[h] = (int64_t)(old & kHubChunkMask);
         if (a.use_hubs == 1)
-          for (int64_t s2 = 0; s2 < k; ++s2) a.hubslot[h * k + s2] = (int32_t)s2;
+          for (int64_t s2 = 0; s2 < k; ++s2) a.hubslot[i * k + s2] = (int32_t)s2;
       }
       a.hub.hubid[i] = h;
     }
@@ -277,7 +277,7 @@ __device__ __forceinline__ void hub_reservoir(const UniformArgs &a, int64_t gw, 
     const int64_t q = c - hstart;
     const uint64_t key = wave_uniform(a.seed * (uint64_t)S + (uint64_t)r);
     const uint2 kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
-    int32_t *sl = a.hubslot + h * k;
+    int32_t *sl = a.hubslot + r * k;
     const uint4 o4a = philox4x32_10(
         make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)lane, 0u), kk);
     const uint4 o4b = philox4x32_10(
@@ -358,9 +358,10 @@ __device__ __forceinline__ void sample_rows(const UniformArgs &a, int64_t blk, i
     }
     return;
   }
-  const int64_t h = use_hubs ? a.hub.hubid[r] : -1;
-  if (h >= 0) {
-    emit_slots(a, S, r, nb, out, a.hubslot + h * k, L);
+  // a hub row (prep's test, from the degree alone: no hub-index load) takes the slots
+  // k_hub_reservoir filled; they are indexed by row
+  if (use_hubs && deg - k > kHubT) {
+    emit_slots(a, S, r, nb, out, a.hubslot + r * k, L);
     return;
   }
   for (int64_t s2 = L; s2 < k; s2 += kGroup) sl[s2] = (int32_t)s2;
