@@ -197,18 +197,18 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_hop(const int64_t *bsum,
   }
 }
 
-// x mod d, exact for 2^11 <= d < 2^30: the fp32 quotient estimate (relative error <= 2^-22,
-// so absolute error <= 2^32 / 2^11 * 2^-22 = 0.5) is within one of floor(x / d), and one
-// 32-bit multiply plus two corrections recover the remainder (the generic % spends four
-// quarter-rate multiplies).  Fuzzed against % over 2^34 pairs on gfx950.
-constexpr uint32_t kModBigMin = 2048;
+// x mod d, exact for 2^12 <= d < 2^30.  x/d < 2^20, and the fp32 estimate x * rcp(d) carries a
+// relative error <= 2^-22 (x and d conversions 2^-24 each, v_rcp_f32 1 ulp), i.e. <= 0.25
+// absolute; the fma's own rounding adds <= 2^-4.  Biased by -0.5, the estimate lies in
+// [x/d - 0.8125, x/d - 0.1875], so its truncation q is floor(x/d) or one less: r = x - q*d is
+// in [0, 2d) and one conditional subtract finishes (the generic % spends four quarter-rate
+// multiplies).  tools/modfuzz.hip: every x for ~1K divisors + 2^34 random pairs, 0 mismatches.
+constexpr uint32_t kModBigMin = 4096;
 __device__ __forceinline__ uint32_t mod_big(uint32_t x, uint32_t d) {
   const float rcp = __builtin_amdgcn_rcpf((float)d);
-  const uint32_t q = (uint32_t)((float)x * rcp);
-  int32_t r = (int32_t)(x - q * d);
-  r = r < 0 ? r + (int32_t)d : r;
-  r = r >= (int32_t)d ? r - (int32_t)d : r;
-  return (uint32_t)r;
+  const uint32_t q = (uint32_t)(int32_t)__builtin_fmaf((float)x, rcp, -0.5f);
+  const uint32_t r = x - q * d;
+  return r >= d ? r - d : r;
 }
 
 // ------------------------------------------------------------------------------------
