@@ -6,7 +6,10 @@ node_classification.py:219-229): P2PCacheSampler._CAPI_sample_node_classifiction
 [15,10,5]) + P2PCacheFeatureServer._CAPI_get_feature(input nodes) +
 ops._CAPI_cuda_index_select(labels, seeds), on a synthetic products-like RMAT graph (configs[1]:
 uniform sampler + full-feature gather, d = 100, whole graph in HBM).  Inputs are resident in HBM
-before the timed region.  N > 1 (torchrun): every rank holds the graph (replicated, weak
+before the timed region.  Batches are prepared by DistGNN.dataloading.PrefetchLoader with
+--depth batches in flight (each on its own stream, over one sampler and one feature server;
+output identical to the sequential loop, which --depth 1 runs); the timed region holds exactly
+K batches.  N > 1 (torchrun): every rank holds the graph (replicated, weak
 scaling, independent replicas) and samples its own slice of the train nids; no collective
 runs in the timed loop.  --shard caches node v on GPU v mod N instead (remote rows read
 one-sided over xGMI through IPC-mapped peer memory).
@@ -54,6 +57,8 @@ def parse():
                         "row is read zero-copy from pinned host memory (SURVEY 8(f) rank 2)")
     p.add_argument("--comm", choices=["gloo", "rccl"], default="gloo",
                    help="transport of the library's setup collectives in --shard mode")
+    p.add_argument("--depth", type=int, default=2,
+                   help="batches in flight (PrefetchLoader streams); 1 = the sequential loop")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--seed", type=int, default=20261015)
@@ -79,7 +84,7 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     import dgs
-    from DistGNN.dataloading import SeedGenerator
+    from DistGNN.dataloading import PrefetchLoader, SeedGenerator
     from DistGNN.dataloading.synthetic import rmat_csc_torch
     if world > 1 and args.shard:
         # setup collectives only (IPC handles, cache lists); the timed loop has none
@@ -153,18 +158,26 @@ def main():
             loader = iter(SeedGenerator(train_local, args.batch, shuffle=True, drop_last=True))
             return next(loader)
 
-    def step():
-        seeds = next_seeds()
-        # the label gather depends only on the seeds: issued first, it runs while the host
-        # enters the sampler (the reference loop's order, node_classification.py:219-229, is
-        # sample -> features -> labels; the three are independent except features <- sample)
+    def step(seeds):
+        """The sequential loop body.  The label gather depends only on the seeds: issued
+        first, it runs while the host enters the sampler (the reference loop's order,
+        node_classification.py:219-229, is sample -> features -> labels)."""
         y = dgs.ops._CAPI_cuda_index_select(labels_dev, seeds)
         blocks = sampler._CAPI_sample_node_classifiction(seeds, fan_out, False)
         x = server._CAPI_get_feature(blocks[-1][1])
-        return sum(b[2].numel() for b in blocks), x.shape[0], x, y, blocks[-1][1]
+        return blocks, x, y
 
-    for _ in range(args.warmup):
-        step()
+    def batches_of(seed_batches):
+        if args.depth == 1:
+            return (step(s) for s in seed_batches)
+        return PrefetchLoader(sampler, seed_batches, fan_out, server=server, labels=labels_dev,
+                              depth=args.depth)
+
+    for _ in batches_of([next_seeds() for _ in range(args.warmup)]):
+        pass
+    # the timed batches' seeds (views of the shuffled train set, as SeedGenerator yields them)
+    timed = [next_seeds() for _ in range(args.steps)]
+    it = batches_of(timed)  # worker threads start here; no batch is submitted before t0
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -174,24 +187,32 @@ def main():
     dgs.ops.profile_enable(dgs.ops.PROFILE_GATHER)
     edges = rows = 0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        e, r, _, _, _ = step()
-        edges += e
-        rows += r
+    last_nids = []
+    for blocks, x, _ in it:
+        edges += sum(b[2].numel() for b in blocks)
+        rows += x.shape[0]
+        if len(last_nids) < 20:
+            last_nids.append(blocks[-1][1])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     prof = dgs.ops.profile_read()
-    # informational, outside the timed region: GPU span of the sample call and label select
-    dgs.ops.profile_enable(dgs.ops.PROFILE_SAMPLE | dgs.ops.PROFILE_SELECT)
-    host_rows = 0.0
-    for _ in range(min(args.steps, 20)):
-        nids = step()[4]
-        host_rows += float((~cached_mask[nids]).sum()) / max(nids.numel(), 1)
-    host_rows /= min(args.steps, 20)
+    host_rows = sum(float((~cached_mask[n.long()]).sum()) / max(n.numel(), 1)
+                    for n in last_nids) / max(len(last_nids), 1)
+    # informational, outside the timed region: the sequential loop's latency per sample call
+    # (host wall, sample + label select) and its GPU span
+    n_side = min(args.steps, 20)
+    side_seeds = [next_seeds() for _ in range(n_side)]
     torch.cuda.synchronize()
+    dgs.ops.profile_enable(dgs.ops.PROFILE_SAMPLE | dgs.ops.PROFILE_SELECT)
+    ts = time.perf_counter()
+    for s in side_seeds:
+        dgs.ops._CAPI_cuda_index_select(labels_dev, s)
+        sampler._CAPI_sample_node_classifiction(s, fan_out, False)
+    torch.cuda.synchronize()
+    seq_ms = (time.perf_counter() - ts) * 1e3 / n_side
     side = dgs.ops.profile_read()
     dgs.ops.profile_enable(False)
 
@@ -245,6 +266,7 @@ def main():
             "fan_out": fan_out, "batch_per_gpu": args.batch, "num_nodes": N, "num_edges": E,
             "feat_dim": args.dim, "parallelism": f"dp{world} (seed-parallel)",
             "cache_frac": args.cache_frac,
+            "pipeline_depth": args.depth,
         },
         "host_row_share": host_rows,
         # host rows cross PCIe Gen5 x16 (63 GB/s spec): their read rate during the gather
@@ -256,6 +278,7 @@ def main():
         "gathered_rows_per_step": rows_all / args.steps,
         "gather_kernel_ms_per_step": prof["gather_ms"] / args.steps,
         "sample_span_ms_per_call": side["sample_ms"] / max(side["sample_calls"], 1),
+        "sequential_sample_ms_per_call": seq_ms,
         "label_select_kernel_ms": side["select_ms"] / max(side["select_launches"], 1),
         "roofline": {
             "bound": "hbm",

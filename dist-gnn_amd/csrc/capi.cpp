@@ -116,6 +116,13 @@ int dgs_allgather_bytes(const void *send, int64_t send_bytes, void *const *recv,
 
 uint64_t dgs_randn_uint64(void) { return rng().next(); }
 
+int dgs_randn_uint64_n(int64_t n, uint64_t *out) {
+  return guard([&] {
+    DGS_CHECK(n >= 0 && (n == 0 || out), "randn_uint64_n: bad arguments");
+    rng().next_n(n, out);
+  });
+}
+
 int dgs_set_random_seed(uint64_t seed) {
   rng().set_seed(seed);
   return 0;
@@ -305,6 +312,20 @@ int dgs_sampler_sample(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
     s->s->sample(dev_ptr(seeds, "seeds"), n_seeds, fan_out, L, replace != 0, frontiers, rows,
                  cols, sizes_out, S(stream));
   });
+}
+
+int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
+                             const int64_t *fan_out, int L, int replace,
+                             int64_t *const *frontiers, int64_t *const *rows,
+                             int64_t *const *cols, const uint64_t *launch_seeds, void *stream) {
+  return guard([&] {
+    s->s->sample_begin(dev_ptr(seeds, "seeds"), n_seeds, fan_out, L, replace != 0, frontiers,
+                       rows, cols, S(stream), launch_seeds);
+  });
+}
+
+int dgs_sampler_sample_end(dgs_sampler *s, int L, int64_t *sizes_out, void *stream) {
+  return guard([&] { s->s->sample_end(L, sizes_out, S(stream)); });
 }
 
 int dgs_sampler_local_cache(const dgs_sampler *s, const int64_t **sub_indptr, int64_t *n_rows,

@@ -160,11 +160,17 @@ void *device_view(const void *p, int64_t bytes, bool *registered_here) {
 }
 
 // ------------------------------------------------------------------ profiler
+// Thread-safe: sampling contexts on several streams may record spans concurrently.
 namespace {
 struct EvPair {
   hipEvent_t a, b;
   int which;
+  hipStream_t st;  // span end matches the open span of the same stream
 };
+std::mutex &prof_mu() {
+  static std::mutex m;
+  return m;
+}
 std::vector<EvPair> &pending() {
   static std::vector<EvPair> v;
   return v;
@@ -194,24 +200,27 @@ Profiler &profiler() {
 KernelEvents profile_kernel(int which) {
   KernelEvents ev;
   if (!profiler().wants(which)) return ev;
+  std::lock_guard<std::mutex> g(prof_mu());
   ev.start = take_event();
   ev.stop = take_event();
-  pending().push_back(EvPair{ev.start, ev.stop, which});
+  pending().push_back(EvPair{ev.start, ev.stop, which, nullptr});
   return ev;
 }
 
 void profile_begin(hipStream_t st, int which) {
   if (!profiler().wants(which)) return;
-  EvPair ev{take_event(), nullptr, which};
+  std::lock_guard<std::mutex> g(prof_mu());
+  EvPair ev{take_event(), nullptr, which, st};
   DGS_HIP(hipEventRecord(ev.a, st));
   pending().push_back(ev);
 }
 
 void profile_end(hipStream_t st, int which) {
   if (!profiler().wants(which)) return;
+  std::lock_guard<std::mutex> g(prof_mu());
   auto &pv = pending();
   for (auto it = pv.rbegin(); it != pv.rend(); ++it) {
-    if (it->which == which && it->b == nullptr) {
+    if (it->which == which && it->b == nullptr && it->st == st) {
       it->b = take_event();
       DGS_HIP(hipEventRecord(it->b, st));
       return;
@@ -220,6 +229,7 @@ void profile_end(hipStream_t st, int which) {
 }
 
 void profile_collect() {
+  std::lock_guard<std::mutex> g(prof_mu());
   auto &pv = pending();
   for (auto &ev : pv) {
     if (!ev.b) continue;

@@ -24,6 +24,11 @@ class RandomEngine {
     std::lock_guard<std::mutex> g(mu_);
     return dis_(gen_);
   }
+  // n consecutive draws under one lock (a multi-hop call's seeds stay contiguous)
+  void next_n(int64_t n, uint64_t *out) {
+    std::lock_guard<std::mutex> g(mu_);
+    for (int64_t i = 0; i < n; ++i) out[i] = dis_(gen_);
+  }
   void set_seed(uint64_t s) {
     std::lock_guard<std::mutex> g(mu_);
     gen_.seed(s);

@@ -157,7 +157,8 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
 }
 
 Sampler::~Sampler() {
-  if (seq_ > 0) (void)hipStreamSynchronize(last_stream_);  // last relabel pass may still run
+  for (auto &kv : ctxs_)  // each context's last relabel pass may still run
+    if (kv.second->seq > 0) (void)hipStreamSynchronize(kv.second->stream);
   delete indptr_srv_;
   delete indices_srv_;
   delete probs_srv_;
@@ -179,31 +180,61 @@ void Sampler::bounds(int64_t n_seeds, const int64_t *fan_out, int L, int64_t *fc
   }
 }
 
+Sampler::Ctx &Sampler::ctx_for(hipStream_t st) {
+  std::lock_guard<std::mutex> g(ctx_mu_);
+  std::unique_ptr<Ctx> &c = ctxs_[st];
+  if (!c) {
+    c.reset(new Ctx);
+    c->stream = st;
+  }
+  return *c;
+}
+
 // sampler.cc:14-62, 146-166: hops run fan_out[L-1] .. fan_out[0]; seeds <- frontier.
 // All hops are enqueued without host synchronisation: hop h+1 reads its seed count from the
 // device word the relabel of hop h wrote, grids are sized by the host-side upper bounds, and
-// the per-hop sizes come back in one D2H copy at the end.
+// the per-hop sizes are published to pinned host memory by the last kernel.
 void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_out, int L,
                      bool replace, int64_t *const *frontiers, int64_t *const *rows,
-                     int64_t *const *cols, int64_t *sizes, hipStream_t st) {
+                     int64_t *const *cols, int64_t *sizes, hipStream_t st,
+                     const uint64_t *launch_seeds) {
   if (L <= 0) return;
+  sample_begin(seeds, n_seeds, fan_out, L, replace, frontiers, rows, cols, st, launch_seeds);
+  sample_end(L, sizes, st);
+}
+
+// Enqueues every hop of one call on `st` and returns: the call's sizes are read by
+// sample_end.  One call per stream may be outstanding (its context holds the published sizes).
+void Sampler::sample_begin(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_out,
+                           int L, bool replace, int64_t *const *frontiers,
+                           int64_t *const *rows, int64_t *const *cols, hipStream_t st,
+                           const uint64_t *launch_seeds) {
+  DGS_CHECK(L > 0, "sample: empty fan_out");
+  for (int h = 0; h < L; ++h) DGS_CHECK(fan_out[h] >= 0, "fan_out entries must be non-negative");
+  // One launch seed per hop (rowwise_sampling.cu:162), drawn together so that concurrent calls
+  // on other streams cannot interleave with this call's draws.
+  std::vector<uint64_t> hop_seed(L);
+  if (launch_seeds)
+    std::copy(launch_seeds, launch_seeds + L, hop_seed.begin());
+  else
+    rng().next_n(L, hop_seed.data());
+  Ctx &c = ctx_for(st);
+  std::lock_guard<std::mutex> g(c.mu);
+  DGS_CHECK(!c.pending, "sample: the previous call on this stream has not been ended");
   // device sizes: 3 per hop, then the bad-seed word (holds the seq of the last call that saw
   // a seed outside [0, num_nodes); zeroed at allocation, never reset)
-  if (sizes_.ensure(sizeof(int64_t) * (size_t)(3 * L + 1)))
-    DGS_HIP(hipMemsetAsync(sizes_.p, 0, sizes_.bytes, st));
-  if (sizes_host_.bytes < sizeof(int64_t) * (size_t)(3 * L + 2)) {
-    sizes_host_.flags = hipHostMallocCoherent | hipHostMallocMapped;
-    sizes_host_.ensure(sizeof(int64_t) * (size_t)(3 * L + 2));
-    sizes_host_.as<int64_t>()[0] = 0;
-    DGS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&sizes_host_dev_), sizes_host_.p, 0));
+  if (c.sizes.ensure(sizeof(int64_t) * (size_t)(3 * L + 1)))
+    DGS_HIP(hipMemsetAsync(c.sizes.p, 0, c.sizes.bytes, st));
+  if (c.sizes_host.bytes < sizeof(int64_t) * (size_t)(3 * L + 2)) {
+    c.sizes_host.flags = hipHostMallocCoherent | hipHostMallocMapped;
+    c.sizes_host.ensure(sizeof(int64_t) * (size_t)(3 * L + 2));
+    c.sizes_host.as<int64_t>()[0] = 0;
+    DGS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.sizes_host_dev),
+                                    c.sizes_host.p, 0));
   }
-  int64_t *dsz = sizes_.as<int64_t>();
-  int64_t *hsz = sizes_host_.as<int64_t>();
-  // The previous call may still be relabelling on its stream (see the wait below): a call on
-  // another stream first drains it, since both use this sampler's scratch.
-  if (seq_ > 0 && st != last_stream_) DGS_HIP(hipStreamSynchronize(last_stream_));
-  last_stream_ = st;
-  const uint64_t seq = ++seq_;
+  int64_t *dsz = c.sizes.as<int64_t>();
+  // (the previous call on this stream may still be relabelling: stream order covers it)
+  const uint64_t seq = ++c.seq;
   RowSrc src = src_;
   src.bad = dsz + 3 * L;
   src.bad_tag = (int64_t)seq;
@@ -219,32 +250,45 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
   bool have_tail = false;
   for (int h = 0; h < L; ++h) {
     const int64_t k = fan_out[L - 1 - h];
-    DGS_CHECK(k >= 0, "fan_out entries must be non-negative");
-    const uint64_t seed = rng().next();
+    const uint64_t seed = hop_seed[h];
     const int64_t nnz_cap = ecap[h];
     int64_t *d_nnz = dsz + 3 * h + 2;
     int64_t *d_uniq = dsz + 3 * h + 1;
     const int tb = h & 1;
-    const Table t = direct_table(dval_[tb], dlab_[tb], num_nodes_, &dtab_dirty_[tb], st);
-    dtab_dirty_[tb] = true;
+    const Table t = direct_table(c.dval[tb], c.dlab[tb], num_nodes_, &c.dirty[tb], st);
+    c.dirty[tb] = true;
     // rows[h] receives each edge's seed row r from the sampler and is relabelled in place
-    sample_hop(src, cur, S, k, replace, bias_, seed, rows[h], cols[h], d_nnz, t, ws_, st,
+    sample_hop(src, cur, S, k, replace, bias_, seed, rows[h], cols[h], d_nnz, t, c.ws, st,
                have_tail ? &tail : nullptr);
-    if (have_tail) dtab_dirty_[tb ^ 1] = false;  // the previous hop's clean-up is enqueued
+    if (have_tail) c.dirty[tb ^ 1] = false;  // the previous hop's clean-up is enqueued
     // the last hop's scatter publishes every size to pinned host memory (no copy, no sync)
     const bool last = h == L - 1;
-    const HostSizes pub = last ? HostSizes{dsz, 3 * L + 1, sizes_host_dev_, seq} : HostSizes{};
+    const HostSizes pub = last ? HostSizes{dsz, 3 * L + 1, c.sizes_host_dev, seq} : HostSizes{};
     relabel_hop(cur, S, cols[h], d_nnz, nnz_cap, /*seeds_unique=*/h > 0, t, frontiers[h],
-                rows[h], cols[h], d_uniq, ws_, st, pub, last ? nullptr : &tail);
+                rows[h], cols[h], d_uniq, c.ws, st, pub, last ? nullptr : &tail);
     have_tail = !last;
-    if (last) dtab_dirty_[tb] = false;
+    if (last) c.dirty[tb] = false;
     cur = frontiers[h];
     S = Count{fcap[h], d_uniq};
   }
   profile_end(st, 1);
-  // Wait for the published sizes only: the host returns while the last relabel pass still runs
-  // (every consumer of the outputs is ordered after it on the stream).  A failed kernel shows
-  // up through hipStreamQuery.
+  c.pending = true;
+  c.pending_L = L;
+  c.pending_seeds = n_seeds;
+}
+
+// Waits for the sizes of the call begun on `st` (published by its last scatter kernel): the
+// host returns while the last relabel pass still runs (every consumer of the outputs is
+// ordered after it on the stream).  A failed kernel shows up through hipStreamQuery.
+void Sampler::sample_end(int L, int64_t *sizes, hipStream_t st) {
+  Ctx &c = ctx_for(st);
+  std::lock_guard<std::mutex> g(c.mu);
+  DGS_CHECK(c.pending, "sample_end: no call outstanding on this stream");
+  DGS_CHECK(L == c.pending_L, "sample_end: hop count differs from the call's");
+  c.pending = false;
+  const int64_t *hsz = c.sizes_host.as<int64_t>();
+  const uint64_t seq = c.seq;
+  const int64_t n_seeds = c.pending_seeds;
   for (uint64_t spin = 1;; ++spin) {
     if (__atomic_load_n(hsz, __ATOMIC_ACQUIRE) == (int64_t)seq) break;
     if ((spin & 255) == 0) {

@@ -4,6 +4,9 @@
 #pragma once
 
 #include <algorithm>
+#include <memory>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "context.h"
@@ -58,9 +61,16 @@ class Sampler {
   ~Sampler();
   void bounds(int64_t n_seeds, const int64_t *fan_out, int L, int64_t *fcap,
               int64_t *ecap) const;
+  // launch_seeds: L per-hop seeds, or nullptr to draw them from the global engine
   void sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_out, int L,
               bool replace, int64_t *const *frontiers, int64_t *const *rows,
-              int64_t *const *cols, int64_t *sizes, hipStream_t st);
+              int64_t *const *cols, int64_t *sizes, hipStream_t st,
+              const uint64_t *launch_seeds = nullptr);
+  // sample() in two halves: enqueue every hop, then wait for the published sizes
+  void sample_begin(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_out, int L,
+                    bool replace, int64_t *const *frontiers, int64_t *const *rows,
+                    int64_t *const *cols, hipStream_t st, const uint64_t *launch_seeds);
+  void sample_end(int L, int64_t *sizes, hipStream_t st);
   const int64_t *sub_indptr() const { return (const int64_t *)indptr_srv_->local(); }
   int64_t n_rows() const { return indptr_srv_->items(rank_) - 1; }
   const int64_t *sub_indices() const { return (const int64_t *)indices_srv_->local(); }
@@ -81,14 +91,25 @@ class Sampler {
   P2PServer *nids_srv_ = nullptr;
   DevBuf ntab_;
   RowSrc src_{};
-  HopScratch ws_;
-  DevBuf dval_[2], dlab_[2];  // direct relabel tables over node ids (first position, label),
-  bool dtab_dirty_[2] = {false, false};  // used by alternate hops
-  DevBuf sizes_;
-  HostPinned sizes_host_;  // [0] publication sequence, [1..3L] per-hop sizes
-  int64_t *sizes_host_dev_ = nullptr;
-  uint64_t seq_ = 0;
-  hipStream_t last_stream_ = nullptr;
+  // Per-stream sampling state: calls on different streams run concurrently over the shared
+  // (read-only) graph; calls on one stream take turns on its context.
+  struct Ctx {
+    std::mutex mu;
+    HopScratch ws;
+    DevBuf dval[2], dlab[2];  // direct relabel tables over node ids (first position, label),
+    bool dirty[2] = {false, false};  // used by alternate hops
+    DevBuf sizes;
+    HostPinned sizes_host;  // [0] publication sequence, [1..3L] per-hop sizes, [3L+1] bad seed
+    int64_t *sizes_host_dev = nullptr;
+    uint64_t seq = 0;
+    hipStream_t stream = nullptr;
+    bool pending = false;  // a call was begun and not yet ended
+    int pending_L = 0;
+    int64_t pending_seeds = 0;
+  };
+  Ctx &ctx_for(hipStream_t st);
+  std::mutex ctx_mu_;
+  std::unordered_map<hipStream_t, std::unique_ptr<Ctx>> ctxs_;
 };
 
 class FeatureServer {

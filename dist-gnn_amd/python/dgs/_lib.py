@@ -41,6 +41,7 @@ _SIGS = {
     "dgs_allgather_sizes": (c_int, [c_i64, p_i64]),
     "dgs_allgather_bytes": (c_int, [c_vp, c_i64, p_vp, p_i64, c_vp]),
     "dgs_randn_uint64": (c_u64, []),
+    "dgs_randn_uint64_n": (c_int, [c_i64, ctypes.POINTER(c_u64)]),
     "dgs_set_random_seed": (c_int, [c_u64]),
     "dgs_host_register": (c_int, [c_vp, c_i64]),
     "dgs_host_unregister": (c_int, [c_vp]),
@@ -61,6 +62,9 @@ _SIGS = {
     "dgs_sampler_bounds": (c_int, [c_vp, c_i64, p_i64, c_int, p_i64, p_i64]),
     "dgs_sampler_sample": (c_int, [c_vp, c_vp, c_i64, p_i64, c_int, c_int, p_vp, p_vp, p_vp,
                                    p_i64, c_vp]),
+    "dgs_sampler_sample_begin": (c_int, [c_vp, c_vp, c_i64, p_i64, c_int, c_int, p_vp, p_vp,
+                                         p_vp, ctypes.POINTER(c_u64), c_vp]),
+    "dgs_sampler_sample_end": (c_int, [c_vp, c_int, p_i64, c_vp]),
     "dgs_sampler_local_cache": (c_int, [c_vp, p_vp, p_i64, p_vp, p_i64, p_vp]),
     "dgs_sampler_cache_map_size": (c_int, [c_vp, p_i64]),
     "dgs_sampler_cache_map_fill": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -95,13 +95,50 @@ class P2PCacheSampler:
 
     def _CAPI_sample_node_classifiction(self, seeds, fan_out, replace=False):
         """sampler.cc:146-166 -> [(seeds, frontier, coo_row, coo_col)] per hop
-        (hop h samples fan_out[L-1-h]); coo ids are local to (frontier, seeds)."""
+        (hop h samples fan_out[L-1-h]); coo ids are local to (frontier, seeds).  Runs on the
+        current stream; calls on different streams run concurrently."""
+        return self._sample(seeds, fan_out, replace, None)
+
+    def _sample_seeded(self, seeds, fan_out, replace, launch_seeds):
+        """ADDITIVE: the same call with caller-drawn per-hop launch seeds (hop h uses
+        launch_seeds[h]; draw them with dgs.ops.draw_launch_seeds)."""
+        return self._sample_begin(seeds, fan_out, replace, launch_seeds).result()
+
+    def _sample_begin(self, seeds, fan_out, replace=False, launch_seeds=None):
+        """ADDITIVE: enqueue the whole call on the current stream and return at once; the
+        returned handle's result() waits for the sizes and gives the call's blocks.  One call
+        per stream may be outstanding (DistGNN.dataloading.PrefetchLoader keeps one per
+        stream on several streams)."""
+        if launch_seeds is not None and len(launch_seeds) != len(fan_out):
+            raise RuntimeError("launch_seeds needs one seed per hop")
+        s, L, fo, caps, total, buf, ptrs = self._prepare(seeds, fan_out)
+        st = stream_ptr(s.device)
+        ls = None
+        if L and launch_seeds is not None:
+            ls = (ctypes.c_uint64 * L)(*[int(x) & 0xFFFFFFFFFFFFFFFF for x in launch_seeds])
+        if L:
+            check(lib.dgs_sampler_sample_begin(self._h, c_vp(s.data_ptr()), s.numel(), fo, L,
+                                               int(bool(replace)), *ptrs, ls, st))
+        return _PendingSample(self, seeds, s, L, caps, total, buf, st)
+
+    def _sample(self, seeds, fan_out, replace, launch_seeds):
+        if launch_seeds is not None:
+            return self._sample_seeded(seeds, fan_out, replace, launch_seeds)
+        s, L, fo, caps, total, buf, ptrs = self._prepare(seeds, fan_out)
+        if L == 0:
+            return []
+        sizes = (c_i64 * (3 * L))()
+        check(lib.dgs_sampler_sample(self._h, c_vp(s.data_ptr()), s.numel(), fo, L,
+                                     int(bool(replace)), *ptrs, sizes, stream_ptr(s.device)))
+        return self._views(seeds, buf, caps, total, sizes, L)
+
+    def _prepare(self, seeds, fan_out):
         check_cuda(seeds, "seeds")
         s = seeds if seeds.dtype == torch.int64 and seeds.is_contiguous() else \
             as_i64(seeds, "seeds")
         L = len(fan_out)
         if L == 0:
-            return []
+            return s, 0, None, [], 0, None, None
         key = (tuple(fan_out), s.numel())
         plan = self._plans.get(key)
         if plan is None:
@@ -114,12 +151,9 @@ class P2PCacheSampler:
         fo, caps, total = plan
         # one allocation for every hop's (frontier, row, col) buffers
         buf = torch.empty(max(total, 1), dtype=torch.int64, device=s.device)
-        base = buf.data_ptr()
-        fr_p, row_p, col_p = plan_ptrs(base, caps)
-        sizes = (c_i64 * (3 * L))()
-        check(lib.dgs_sampler_sample(self._h, c_vp(s.data_ptr()), s.numel(), fo, L,
-                                     int(bool(replace)), fr_p, row_p, col_p, sizes,
-                                     stream_ptr(s.device)))
+        return s, L, fo, caps, total, buf, plan_ptrs(buf.data_ptr(), caps)
+
+    def _views(self, seeds, buf, caps, total, sizes, L):
         # all views in one split: [U_h, pad, nnz_h, pad, nnz_h, pad] per hop
         lens = []
         for h, (f, e) in enumerate(caps):
@@ -228,3 +262,25 @@ class P2PCacheFeatureServer:
         if h is not None and h.value:
             lib.dgs_feature_server_destroy(h)
             self._h = None
+
+
+class _PendingSample:
+    """A sample call enqueued by P2PCacheSampler._sample_begin; result() (once) waits for the
+    sizes its last kernel publishes and returns the per-hop (seeds, frontier, row, col)."""
+
+    def __init__(self, owner, seeds, s64, L, caps, total, buf, stream):
+        self._owner, self._seeds, self._s64 = owner, seeds, s64
+        self._L, self._caps, self._total, self._buf, self._stream = L, caps, total, buf, stream
+        self._out = None
+
+    def result(self):
+        if self._out is None:
+            if self._L == 0:
+                self._out = []
+            else:
+                sizes = (c_i64 * (3 * self._L))()
+                check(lib.dgs_sampler_sample_end(self._owner._h, self._L, sizes, self._stream))
+                self._out = self._owner._views(self._seeds, self._buf, self._caps, self._total,
+                                               sizes, self._L)
+            self._s64 = self._buf = None
+        return self._out

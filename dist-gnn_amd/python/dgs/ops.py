@@ -18,7 +18,7 @@ __all__ = [
     "_CAPI_cuda_sample_neighbors_bias", "_CAPI_cuda_sampled_tensor_relabel",
     "_CAPI_cuda_index_select", "_Test_Randn", "_Test_NCCLTensorAllGather",
     "_Test_GetLocalRank", "_Test_GetWorldSize", "_Test_ExtractEdgeData", "_Test_ExtractIndptr",
-    "_CAPI_set_random_seed", "_CAPI_set_host_comm",
+    "_CAPI_set_random_seed", "_CAPI_set_host_comm", "draw_launch_seeds",
 ]
 
 _registered = {}
@@ -91,6 +91,14 @@ def _Test_GetWorldSize():
 def _Test_Randn():
     """context/context.h:22-27 -- next launch seed (uint64)."""
     return int(lib.dgs_randn_uint64())
+
+
+def draw_launch_seeds(n):
+    """ADDITIVE: the next n launch seeds of the global engine, drawn under one lock (what one
+    n-hop sample call would draw), for P2PCacheSampler._sample_seeded."""
+    out = (ctypes.c_uint64 * int(n))()
+    check(lib.dgs_randn_uint64_n(int(n), out))
+    return [int(x) for x in out]
 
 
 def _CAPI_set_random_seed(seed):

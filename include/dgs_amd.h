@@ -59,6 +59,9 @@ int dgs_allgather_bytes(const void *send, int64_t send_bytes, void *const *recv 
                         const int64_t *recv_bytes /* [world] */, void *stream);
 /* replaces ctx::randn_uint64 (context/context.h:22-27; pybind.cc:71 _Test_Randn) */
 uint64_t dgs_randn_uint64(void);
+/* ADDITIVE: n consecutive draws of the same engine under one lock (the seeds one
+ * dgs_sampler_sample call would draw, for dgs_sampler_sample_seeded). */
+int dgs_randn_uint64_n(int64_t n, uint64_t *out);
 /* ADDITIVE (not in the reference): reseed the launch-seed engine (std::mt19937_64) so that
  * sampling is reproducible; the reference seeds it from std::random_device
  * (context/context.h:9-10). */
@@ -146,11 +149,25 @@ int dgs_sampler_bounds(const dgs_sampler *s, int64_t n_seeds, const int64_t *fan
 /* replaces P2PCacheSampler::NodeClassifictionSample (sampler.cc:146-166): hop h writes the
  * frontier (unique(seeds_h ++ sampled cols), first-occurrence order) to frontiers[h] and the
  * relabeled COO to rows[h]/cols[h]; sizes_out[3h..3h+2] = (S_h, |frontier_h|, nnz_h).
- * SYNC (once per hop). */
+ * One launch seed per hop comes from the global engine (rowwise_sampling.cu:162).  The host
+ * waits once, for the sizes the last kernel publishes; the last relabel pass may still run on
+ * `stream` when the call returns.  Calls on different streams run concurrently (each stream
+ * has its own sampling context over the shared graph). */
 int dgs_sampler_sample(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
                        const int64_t *fan_out, int L, int replace, int64_t *const *frontiers,
                        int64_t *const *rows, int64_t *const *cols, int64_t *sizes_out,
                        void *stream);
+/* ADDITIVE: dgs_sampler_sample in two halves.  _begin enqueues every hop on `stream` and
+ * returns without waiting; _end waits for that call's sizes (same `stream`, same L).  At most
+ * one call per stream is outstanding.  launch_seeds: the L per-hop launch seeds (hop h uses
+ * launch_seeds[h]), or NULL to draw them from the global engine; a pipelined loader draws
+ * them with dgs_randn_uint64_n in batch order, so overlapped calls on several streams give
+ * exactly the results of sequential dgs_sampler_sample calls. */
+int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
+                             const int64_t *fan_out, int L, int replace,
+                             int64_t *const *frontiers, int64_t *const *rows,
+                             int64_t *const *cols, const uint64_t *launch_seeds, void *stream);
+int dgs_sampler_sample_end(dgs_sampler *s, int L, int64_t *sizes_out, void *stream);
 /* _CAPI_get_local_cache_structure_tensors (sampler.cc:183-195): non-owning device views. */
 int dgs_sampler_local_cache(const dgs_sampler *s, const int64_t **sub_indptr, int64_t *n_rows,
                             const int64_t **sub_indices, int64_t *n_edges,

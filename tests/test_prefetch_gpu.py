@@ -1,0 +1,162 @@
+"""Pipelined batch preparation (DistGNN.dataloading.PrefetchLoader) and the per-stream sampling
+contexts under it: several batches in flight on separate streams over one sampler must give
+exactly the sequential loop's blocks, features and labels (bit-exact), and the seeded entry
+point must reproduce the engine-drawn call."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dgs():
+    import dgs as _dgs
+    return _dgs
+
+
+def _graph(seed=3, n=3000):
+    rng = np.random.default_rng(seed)
+    degs = rng.integers(0, 60, n)
+    degs[:4] = [0, 5, 4000, 700]  # empty row, deg < k, uniform hubs on both modulo paths
+    indptr = np.concatenate([[0], np.cumsum(degs)]).astype(np.int64)
+    indices = rng.integers(0, n, int(indptr[-1])).astype(np.int64)
+    probs = (rng.random(indices.size) + 0.01).astype(np.float32)
+    return indptr, indices, probs
+
+
+def _services(dgs, bias, id_dtype=torch.int64, dim=33):
+    indptr, indices, probs = _graph()
+    n = indptr.size - 1
+    ip, ix = torch.from_numpy(indptr).to(id_dtype), torch.from_numpy(indices).to(id_dtype)
+    pr = torch.from_numpy(probs) if bias else torch.Tensor()
+    sampler = dgs.classes.P2PCacheSampler(ip, ix, pr, torch.arange(0, n, 3), 0)
+    feats = torch.arange(n * dim, dtype=torch.float32).reshape(n, dim)
+    server = dgs.classes.P2PCacheFeatureServer(feats, torch.arange(1, n, 2), 0)
+    labels = torch.randint(0, 40, (n,), generator=torch.Generator().manual_seed(0)).cuda()
+    return (indptr, indices, probs), sampler, server, labels, feats
+
+
+def _batches(n, nb=12, bsz=64, id_dtype=torch.int64):
+    g = torch.Generator().manual_seed(9)
+    out = [torch.randint(0, n, (bsz,), generator=g) for _ in range(nb)]
+    out[min(1, nb - 1)][:4] = torch.tensor([0, 1, 2, 3])  # the special rows in one batch
+    return [b.to(id_dtype).cuda() for b in out]
+
+
+def _sequential(dgs, sampler, server, labels, batches, fan_out):
+    out = []
+    for s in batches:
+        blocks = sampler._CAPI_sample_node_classifiction(s, fan_out, False)
+        x = server._CAPI_get_feature(blocks[-1][1])
+        y = dgs.ops._CAPI_cuda_index_select(labels, s)
+        out.append((blocks, x, y))
+    return out
+
+
+def _same(a, b):
+    (ba, xa, ya), (bb, xb, yb) = a, b
+    assert len(ba) == len(bb)
+    for ta, tb in zip(ba, bb):
+        for u, v in zip(ta, tb):
+            assert u.dtype == v.dtype and torch.equal(u, v)
+    assert torch.equal(xa, xb) and torch.equal(ya, yb)
+
+
+@pytest.mark.parametrize("depth", [1, 2, 4])
+@pytest.mark.parametrize("bias", [False, True])
+def test_prefetch_matches_sequential(dgs, depth, bias):
+    from DistGNN.dataloading import PrefetchLoader
+    _, sampler, server, labels, _ = _services(dgs, bias)
+    fan_out = [8, 5, 3] if bias else [15, 10, 5]
+    batches = _batches(labels.numel())
+    dgs.ops._CAPI_set_random_seed(77)
+    exp = _sequential(dgs, sampler, server, labels, batches, fan_out)
+    dgs.ops._CAPI_set_random_seed(77)
+    got = list(PrefetchLoader(sampler, batches, fan_out, server=server, labels=labels,
+                              depth=depth))
+    torch.cuda.synchronize()
+    assert len(got) == len(exp)
+    for g, e in zip(got, exp):
+        _same(g, e)
+
+
+def test_prefetch_int32_ids_and_oracle(dgs):
+    """int32 graph ids (cast outputs), and the pipelined blocks against the CPU oracle."""
+    from DistGNN.dataloading import PrefetchLoader
+    (indptr, indices, _), sampler, server, labels, feats = _services(dgs, False, torch.int32)
+    fan_out = [10, 4]
+    batches = _batches(labels.numel(), nb=6, id_dtype=torch.int32)
+    dgs.ops._CAPI_set_random_seed(5)
+    got = list(PrefetchLoader(sampler, batches, fan_out, server=server, labels=labels, depth=3))
+    allseeds = O.launch_seeds(5, 2 * len(batches))  # the engine's sequence, 2 per batch
+    for i, (s, (blocks, x, y)) in enumerate(zip(batches, got)):
+        exp = O.node_classification_sample(s.cpu().numpy().astype(np.int64), indptr, indices,
+                                           fan_out, False, allseeds[2 * i:2 * i + 2])
+        for (gs, gf, gr, gc), (es, ef, er, ec) in zip(blocks, exp):
+            assert gf.dtype == torch.int32
+            assert np.array_equal(gf.cpu().numpy(), ef)
+            assert np.array_equal(gr.cpu().numpy(), er)
+            assert np.array_equal(gc.cpu().numpy(), ec)
+        assert torch.equal(x.cpu(), feats[blocks[-1][1].long().cpu()])
+        assert torch.equal(y, labels[s.long()])
+
+
+def test_seeded_call_equals_engine_call(dgs):
+    _, sampler, _, labels, _ = _services(dgs, False)
+    s = _batches(labels.numel(), nb=1)[0]
+    dgs.ops._CAPI_set_random_seed(123)
+    a = sampler._CAPI_sample_node_classifiction(s, [15, 10, 5], False)
+    dgs.ops._CAPI_set_random_seed(123)
+    ls = dgs.ops.draw_launch_seeds(3)
+    b = sampler._sample_seeded(s, [15, 10, 5], False, ls)
+    for ta, tb in zip(a, b):
+        for u, v in zip(ta, tb):
+            assert torch.equal(u, v)
+    with pytest.raises(RuntimeError):
+        sampler._sample_seeded(s, [15, 10, 5], False, ls[:2])
+
+
+def test_concurrent_streams_share_one_sampler(dgs):
+    """Two streams sampling at once through one sampler (no loader): each stream's results
+    equal the same seeded call made alone."""
+    import threading
+    _, sampler, _, labels, _ = _services(dgs, False)
+    batches = _batches(labels.numel(), nb=8)
+    seeds = [dgs.ops.draw_launch_seeds(3) for _ in batches]
+    exp = [sampler._sample_seeded(s, [15, 10, 5], False, ls) for s, ls in zip(batches, seeds)]
+    torch.cuda.synchronize()
+    got = [None] * len(batches)
+
+    def run(w):
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            for i in range(w, len(batches), 2):
+                got[i] = sampler._sample_seeded(batches[i], [15, 10, 5], False, seeds[i])
+            st.synchronize()
+
+    ths = [threading.Thread(target=run, args=(w,)) for w in range(2)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for g, e in zip(got, exp):
+        for ta, tb in zip(g, e):
+            for u, v in zip(ta, tb):
+                assert torch.equal(u, v)
+
+
+def test_prefetch_propagates_errors_in_order(dgs):
+    from DistGNN.dataloading import PrefetchLoader
+    _, sampler, server, labels, _ = _services(dgs, False)
+    n = labels.numel()
+    batches = _batches(n, nb=5)
+    batches[3] = batches[3].clone()
+    batches[3][0] = n + 5  # outside [0, num_nodes)
+    it = PrefetchLoader(sampler, batches, [5, 5], server=server, depth=2)
+    for _ in range(3):
+        next(it)
+    with pytest.raises(RuntimeError, match="outside"):
+        next(it)
