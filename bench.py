@@ -57,7 +57,7 @@ def parse():
                         "row is read zero-copy from pinned host memory (SURVEY 8(f) rank 2)")
     p.add_argument("--comm", choices=["gloo", "rccl"], default="gloo",
                    help="transport of the library's setup collectives in --shard mode")
-    p.add_argument("--depth", type=int, default=2,
+    p.add_argument("--depth", type=int, default=3,
                    help="batches in flight (PrefetchLoader streams); 1 = the sequential loop")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -202,18 +202,25 @@ def main():
     host_rows = sum(float((~cached_mask[n.long()]).sum()) / max(n.numel(), 1)
                     for n in last_nids) / max(len(last_nids), 1)
     # informational, outside the timed region: the sequential loop's latency per sample call
-    # (host wall, sample + label select) and its GPU span
+    # (host wall, sample + label select), its GPU span, and the feature gather on its own
     n_side = min(args.steps, 20)
     side_seeds = [next_seeds() for _ in range(n_side)]
     torch.cuda.synchronize()
     dgs.ops.profile_enable(dgs.ops.PROFILE_SAMPLE | dgs.ops.PROFILE_SELECT)
     ts = time.perf_counter()
+    side_nids = []
     for s in side_seeds:
         dgs.ops._CAPI_cuda_index_select(labels_dev, s)
-        sampler._CAPI_sample_node_classifiction(s, fan_out, False)
+        side_nids.append(sampler._CAPI_sample_node_classifiction(s, fan_out, False)[-1][1])
     torch.cuda.synchronize()
     seq_ms = (time.perf_counter() - ts) * 1e3 / n_side
     side = dgs.ops.profile_read()
+    dgs.ops.profile_enable(dgs.ops.PROFILE_GATHER)
+    iso_rows = 0
+    for n in side_nids:
+        iso_rows += server._CAPI_get_feature(n).shape[0]
+    torch.cuda.synchronize()
+    iso = dgs.ops.profile_read()
     dgs.ops.profile_enable(False)
 
     row_bytes = args.dim * 4
@@ -285,11 +292,22 @@ def main():
             "kernel": ("k_gather<16, StridedSrc> (P2PCacheFeatureServer gather, computed row "
                        "addresses)" if layout >= 0 else
                        "k_gather<16, TableSrc> (P2PCacheFeatureServer gather, address table)"),
-            "timing": "hipExtLaunchKernelGGL start/stop events (GPU-side kernel start/end)",
+            "timing": ("hipExtLaunchKernelGGL start/stop events (GPU-side kernel start/end) "
+                       "over the timed region, where each gather shares the GPU with the "
+                       "sampling kernels of the other batches in flight"),
             "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "bytes_per_launch": g_bytes, "avg_launch_ms": g_ms,
             "traffic": traffic,
+        },
+        # the same gather kernel with nothing running beside it (sequential side pass)
+        "roofline_isolated": {
+            "achieved": (iso_rows * (2 * args.dim * 4 + 8) / (iso["gather_ms"] * 1e-3) / 1e9
+                         if iso["gather_ms"] > 0 else 0.0),
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": (iso_rows * (2 * args.dim * 4 + 8) / (iso["gather_ms"] * 1e-3) / 1e9
+                     / HBM_PEAK_GBPS if iso["gather_ms"] > 0 else 0.0),
+            "avg_launch_ms": iso["gather_ms"] / max(iso["gather_launches"], 1),
         },
         "cpu_baseline": cpu,
     }

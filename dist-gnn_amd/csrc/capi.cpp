@@ -317,10 +317,12 @@ int dgs_sampler_sample(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
 int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
                              const int64_t *fan_out, int L, int replace,
                              int64_t *const *frontiers, int64_t *const *rows,
-                             int64_t *const *cols, const uint64_t *launch_seeds, void *stream) {
+                             int64_t *const *cols, const uint64_t *launch_seeds, int flags,
+                             void *stream) {
   return guard([&] {
+    DGS_CHECK((flags & ~DGS_SAMPLE_HOST_ASYNC) == 0, "sample_begin: unknown flags");
     s->s->sample_begin(dev_ptr(seeds, "seeds"), n_seeds, fan_out, L, replace != 0, frontiers,
-                       rows, cols, S(stream), launch_seeds);
+                       rows, cols, S(stream), launch_seeds, (flags & DGS_SAMPLE_HOST_ASYNC) != 0);
   });
 }
 

@@ -157,8 +157,18 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
 }
 
 Sampler::~Sampler() {
-  for (auto &kv : ctxs_)  // each context's last relabel pass may still run
-    if (kv.second->seq > 0) (void)hipStreamSynchronize(kv.second->stream);
+  for (auto &kv : ctxs_) {
+    Ctx &c = *kv.second;
+    if (c.launcher.joinable()) {
+      {
+        std::lock_guard<std::mutex> g(c.mu);
+        c.stop = true;
+      }
+      c.cv.notify_all();
+      c.launcher.join();
+    }
+    if (c.seq > 0) (void)hipStreamSynchronize(c.stream);  // the last relabel pass may still run
+  }
   delete indptr_srv_;
   delete indices_srv_;
   delete probs_srv_;
@@ -208,19 +218,87 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
 void Sampler::sample_begin(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_out,
                            int L, bool replace, int64_t *const *frontiers,
                            int64_t *const *rows, int64_t *const *cols, hipStream_t st,
-                           const uint64_t *launch_seeds) {
+                           const uint64_t *launch_seeds, bool host_async) {
   DGS_CHECK(L > 0, "sample: empty fan_out");
   for (int h = 0; h < L; ++h) DGS_CHECK(fan_out[h] >= 0, "fan_out entries must be non-negative");
-  // One launch seed per hop (rowwise_sampling.cu:162), drawn together so that concurrent calls
-  // on other streams cannot interleave with this call's draws.
-  std::vector<uint64_t> hop_seed(L);
-  if (launch_seeds)
-    std::copy(launch_seeds, launch_seeds + L, hop_seed.begin());
-  else
-    rng().next_n(L, hop_seed.data());
+  Job j;
+  j.seeds = seeds;
+  j.n_seeds = n_seeds;
+  j.L = L;
+  j.replace = replace;
+  j.fan_out.assign(fan_out, fan_out + L);
+  j.fr.assign(frontiers, frontiers + L);
+  j.rows.assign(rows, rows + L);
+  j.cols.assign(cols, cols + L);
   Ctx &c = ctx_for(st);
-  std::lock_guard<std::mutex> g(c.mu);
+  std::unique_lock<std::mutex> lk(c.mu);
   DGS_CHECK(!c.pending, "sample: the previous call on this stream has not been ended");
+  // One launch seed per hop (rowwise_sampling.cu:162), drawn together so that concurrent calls
+  // on other streams cannot interleave with this call's draws (a rejected call draws none).
+  j.hop_seed.resize(L);
+  if (launch_seeds)
+    std::copy(launch_seeds, launch_seeds + L, j.hop_seed.begin());
+  else
+    rng().next_n(L, j.hop_seed.data());
+  c.pending = true;
+  c.pending_L = L;
+  c.pending_seeds = n_seeds;
+  if (!host_async) {
+    try {
+      launch(c, j, st);
+    } catch (...) {
+      c.pending = false;
+      throw;
+    }
+    return;
+  }
+  // The context's launcher thread issues the launches (about 2.7 us of host time each); the
+  // caller's thread is free at once.  sample_end waits for it.
+  if (!c.launcher.joinable()) {
+    int dev = 0;
+    DGS_HIP(hipGetDevice(&dev));
+    c.launcher = std::thread([this, &c, dev] { launcher_loop(c, dev); });
+  }
+  c.job = std::move(j);
+  c.job_ready = true;
+  c.job_done = false;
+  c.job_err = nullptr;
+  c.cv.notify_all();
+}
+
+void Sampler::launcher_loop(Ctx &c, int dev) {
+  (void)hipSetDevice(dev);
+  std::unique_lock<std::mutex> lk(c.mu);
+  for (;;) {
+    c.cv.wait(lk, [&] { return c.job_ready || c.stop; });
+    if (c.stop) return;
+    c.job_ready = false;
+    Job j = std::move(c.job);
+    lk.unlock();
+    std::exception_ptr err;
+    try {
+      launch(c, j, c.stream);
+    } catch (...) {
+      err = std::current_exception();
+    }
+    lk.lock();
+    c.job_err = err;
+    c.job_done = true;
+    c.cv.notify_all();
+  }
+}
+
+// Enqueues every hop of one call (the caller holds the context: its `pending` flag is set).
+void Sampler::launch(Ctx &c, const Job &j, hipStream_t st) {
+  const int64_t *seeds = j.seeds;
+  const int64_t n_seeds = j.n_seeds;
+  const int L = j.L;
+  const bool replace = j.replace;
+  const int64_t *fan_out = j.fan_out.data();
+  int64_t *const *frontiers = j.fr.data();
+  int64_t *const *rows = j.rows.data();
+  int64_t *const *cols = j.cols.data();
+  const uint64_t *hop_seed = j.hop_seed.data();
   // device sizes: 3 per hop, then the bad-seed word (holds the seq of the last call that saw
   // a seed outside [0, num_nodes); zeroed at allocation, never reset)
   if (c.sizes.ensure(sizeof(int64_t) * (size_t)(3 * L + 1)))
@@ -272,9 +350,6 @@ void Sampler::sample_begin(const int64_t *seeds, int64_t n_seeds, const int64_t 
     S = Count{fcap[h], d_uniq};
   }
   profile_end(st, 1);
-  c.pending = true;
-  c.pending_L = L;
-  c.pending_seeds = n_seeds;
 }
 
 // Waits for the sizes of the call begun on `st` (published by its last scatter kernel): the
@@ -282,10 +357,16 @@ void Sampler::sample_begin(const int64_t *seeds, int64_t n_seeds, const int64_t 
 // ordered after it on the stream).  A failed kernel shows up through hipStreamQuery.
 void Sampler::sample_end(int L, int64_t *sizes, hipStream_t st) {
   Ctx &c = ctx_for(st);
-  std::lock_guard<std::mutex> g(c.mu);
+  std::unique_lock<std::mutex> lk(c.mu);
   DGS_CHECK(c.pending, "sample_end: no call outstanding on this stream");
   DGS_CHECK(L == c.pending_L, "sample_end: hop count differs from the call's");
+  c.cv.wait(lk, [&] { return c.job_done; });  // an asynchronous launch has been issued
   c.pending = false;
+  if (c.job_err) {
+    std::exception_ptr e = c.job_err;
+    c.job_err = nullptr;
+    std::rethrow_exception(e);
+  }
   const int64_t *hsz = c.sizes_host.as<int64_t>();
   const uint64_t seq = c.seq;
   const int64_t n_seeds = c.pending_seeds;

@@ -4,8 +4,11 @@
 #pragma once
 
 #include <algorithm>
+#include <condition_variable>
+#include <exception>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -67,9 +70,12 @@ class Sampler {
               int64_t *const *cols, int64_t *sizes, hipStream_t st,
               const uint64_t *launch_seeds = nullptr);
   // sample() in two halves: enqueue every hop, then wait for the published sizes
+  // (host_async: a per-stream library thread issues the launches; the caller must not use
+  // the stream before sample_end)
   void sample_begin(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_out, int L,
                     bool replace, int64_t *const *frontiers, int64_t *const *rows,
-                    int64_t *const *cols, hipStream_t st, const uint64_t *launch_seeds);
+                    int64_t *const *cols, hipStream_t st, const uint64_t *launch_seeds,
+                    bool host_async = false);
   void sample_end(int L, int64_t *sizes, hipStream_t st);
   const int64_t *sub_indptr() const { return (const int64_t *)indptr_srv_->local(); }
   int64_t n_rows() const { return indptr_srv_->items(rank_) - 1; }
@@ -93,8 +99,22 @@ class Sampler {
   RowSrc src_{};
   // Per-stream sampling state: calls on different streams run concurrently over the shared
   // (read-only) graph; calls on one stream take turns on its context.
+  struct Job {
+    const int64_t *seeds = nullptr;
+    int64_t n_seeds = 0;
+    int L = 0;
+    bool replace = false;
+    std::vector<int64_t> fan_out;
+    std::vector<int64_t *> fr, rows, cols;
+    std::vector<uint64_t> hop_seed;
+  };
   struct Ctx {
     std::mutex mu;
+    std::condition_variable cv;
+    std::thread launcher;  // started by the first host-asynchronous call
+    Job job;
+    bool job_ready = false, job_done = true, stop = false;
+    std::exception_ptr job_err;
     HopScratch ws;
     DevBuf dval[2], dlab[2];  // direct relabel tables over node ids (first position, label),
     bool dirty[2] = {false, false};  // used by alternate hops
@@ -108,6 +128,8 @@ class Sampler {
     int64_t pending_seeds = 0;
   };
   Ctx &ctx_for(hipStream_t st);
+  void launch(Ctx &c, const Job &j, hipStream_t st);
+  void launcher_loop(Ctx &c, int dev);
   std::mutex ctx_mu_;
   std::unordered_map<hipStream_t, std::unique_ptr<Ctx>> ctxs_;
 };

@@ -85,8 +85,10 @@ class PrefetchLoader:
             y = None
             if self.labels is not None:  # depends on the seeds only: issued first
                 y = dgs.ops._CAPI_cuda_index_select(self.labels, seeds)
+            # the stream is not touched again before result(): the sampler's launcher thread
+            # may issue the launches
             pending = self.sampler._sample_begin(seeds, self.fan_out, self.replace,
-                                                 launch_seeds)
+                                                 launch_seeds, host_async=True)
         self._inflight.append((pending, y, st))
 
     def __iter__(self):

@@ -104,11 +104,13 @@ class P2PCacheSampler:
         launch_seeds[h]; draw them with dgs.ops.draw_launch_seeds)."""
         return self._sample_begin(seeds, fan_out, replace, launch_seeds).result()
 
-    def _sample_begin(self, seeds, fan_out, replace=False, launch_seeds=None):
+    def _sample_begin(self, seeds, fan_out, replace=False, launch_seeds=None, host_async=False):
         """ADDITIVE: enqueue the whole call on the current stream and return at once; the
         returned handle's result() waits for the sizes and gives the call's blocks.  One call
         per stream may be outstanding (DistGNN.dataloading.PrefetchLoader keeps one per
-        stream on several streams)."""
+        stream on several streams).  host_async: a library thread issues the launches, so
+        this returns before they are enqueued -- nothing else may be enqueued on the stream
+        until result()."""
         if launch_seeds is not None and len(launch_seeds) != len(fan_out):
             raise RuntimeError("launch_seeds needs one seed per hop")
         s, L, fo, caps, total, buf, ptrs = self._prepare(seeds, fan_out)
@@ -118,7 +120,8 @@ class P2PCacheSampler:
             ls = (ctypes.c_uint64 * L)(*[int(x) & 0xFFFFFFFFFFFFFFFF for x in launch_seeds])
         if L:
             check(lib.dgs_sampler_sample_begin(self._h, c_vp(s.data_ptr()), s.numel(), fo, L,
-                                               int(bool(replace)), *ptrs, ls, st))
+                                               int(bool(replace)), *ptrs, ls,
+                                               1 if host_async else 0, st))
         return _PendingSample(self, seeds, s, L, caps, total, buf, st)
 
     def _sample(self, seeds, fan_out, replace, launch_seeds):

@@ -162,11 +162,16 @@ int dgs_sampler_sample(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
  * one call per stream is outstanding.  launch_seeds: the L per-hop launch seeds (hop h uses
  * launch_seeds[h]), or NULL to draw them from the global engine; a pipelined loader draws
  * them with dgs_randn_uint64_n in batch order, so overlapped calls on several streams give
- * exactly the results of sequential dgs_sampler_sample calls. */
+ * exactly the results of sequential dgs_sampler_sample calls.
+ * flags: DGS_SAMPLE_HOST_ASYNC -- a library thread (one per stream) issues the launches and
+ * _begin returns before they are enqueued; the caller then must not enqueue work on `stream`
+ * until _end returns.  The output buffers and seeds must stay alive until _end. */
+#define DGS_SAMPLE_HOST_ASYNC 1
 int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
                              const int64_t *fan_out, int L, int replace,
                              int64_t *const *frontiers, int64_t *const *rows,
-                             int64_t *const *cols, const uint64_t *launch_seeds, void *stream);
+                             int64_t *const *cols, const uint64_t *launch_seeds, int flags,
+                             void *stream);
 int dgs_sampler_sample_end(dgs_sampler *s, int L, int64_t *sizes_out, void *stream);
 /* _CAPI_get_local_cache_structure_tensors (sampler.cc:183-195): non-owning device views. */
 int dgs_sampler_local_cache(const dgs_sampler *s, const int64_t **sub_indptr, int64_t *n_rows,

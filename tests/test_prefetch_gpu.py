@@ -160,3 +160,27 @@ def test_prefetch_propagates_errors_in_order(dgs):
         next(it)
     with pytest.raises(RuntimeError, match="outside"):
         next(it)
+
+
+@pytest.mark.parametrize("host_async", [False, True])
+def test_begin_end_protocol(dgs, host_async):
+    """One outstanding call per stream; a second begin, or an end without a begin, raises and
+    leaves the context usable."""
+    _, sampler, _, labels, _ = _services(dgs, False)
+    s = _batches(labels.numel(), nb=1)[0]
+    dgs.ops._CAPI_set_random_seed(11)
+    exp = sampler._CAPI_sample_node_classifiction(s, [10, 5], False)
+    dgs.ops._CAPI_set_random_seed(11)
+    p = sampler._sample_begin(s, [10, 5], False, host_async=host_async)
+    with pytest.raises(RuntimeError, match="not been ended"):
+        sampler._sample_begin(s, [10, 5], False, host_async=host_async)
+    got = p.result()
+    for ta, tb in zip(got, exp):
+        for u, v in zip(ta, tb):
+            assert torch.equal(u, v)
+    from dgs._lib import c_i64, lib
+    sizes = (c_i64 * 6)()
+    assert lib.dgs_sampler_sample_end(sampler._h, 2, sizes,
+                                      dgs._lib.stream_ptr(torch.device("cuda", 0))) != 0
+    again = sampler._CAPI_sample_node_classifiction(s, [10, 5], False)
+    assert again[0][1].numel() > 0
