@@ -11,9 +11,9 @@ import sys
 def load(path):
     out = {}
     for r in csv.DictReader(open(path)):
-        n = r['Name']
-        m = re.search(r'(k_\w+)(<[^()]*>)?', n)
-        short = (m.group(1) + (m.group(2) or '')) if m and 'dgs' in n else n[:50]
+        n = r['Name'].replace('dgs::(anonymous namespace)::', '')
+        m = re.search(r'(k_\w+)(<.*?>)?(?=\(|$)', n)
+        short = (m.group(1) + (m.group(2) or '')) if m and 'dgs' in r['Name'] else n[:50]
         t, c, mx = float(r['TotalDurationNs']), int(r['Calls']), float(r['MaxNs'])
         if short in out:
             t0, c0, mx0 = out[short]
