@@ -36,14 +36,17 @@ def main():
                 sys.exit(out.returncode)
             line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
             d = json.loads(line)
+            iso = d.get("roofline_isolated", {}).get("frac", 0.0)
             res[lib].append((d["ms_per_step"], d["sample_span_ms_per_call"],
-                             d["gather_kernel_ms_per_step"]))
+                             d["roofline"]["frac"], iso, d["value"]))
             print(f"round {r} {lib}: {d['ms_per_step'] * 1e3:.1f} us/step "
-                  f"sample span {d['sample_span_ms_per_call'] * 1e3:.1f} us", flush=True)
+                  f"sample span {d['sample_span_ms_per_call'] * 1e3:.1f} us "
+                  f"gather frac {d['roofline']['frac']:.3f} (isolated {iso:.3f})", flush=True)
     for lib, v in res.items():
-        print(f"MEDIAN {lib}: {statistics.median(x[0] for x in v) * 1e3:.1f} us/step, "
-              f"sample span {statistics.median(x[1] for x in v) * 1e3:.1f} us, "
-              f"gather {statistics.median(x[2] for x in v) * 1e3:.1f} us")
+        med = [statistics.median(x[i] for x in v) for i in range(5)]
+        print(f"MEDIAN {lib}: {med[4] / 1e6:.0f} M edges/s, {med[0] * 1e3:.1f} us/step, "
+              f"sample span {med[1] * 1e3:.1f} us, gather frac {med[2]:.3f}, "
+              f"isolated {med[3]:.3f}")
 
 
 if __name__ == "__main__":
