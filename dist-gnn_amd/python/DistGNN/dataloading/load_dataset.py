@@ -15,8 +15,9 @@ def _load(path, name):
 
 def load_dataset(path, dataset_name, with_feature=True, with_probs=False):
     meta = _load(path, "metadata")
+    # the reference asserts (load_dataset.py:9)
     if meta["dataset"] != dataset_name:
-        raise ValueError(f"{path} holds {meta['dataset']}, not {dataset_name}")
+        raise AssertionError(f"{path} holds {meta['dataset']}, not {dataset_name}")
     graph = {name: _load(path, name) for name in ("labels", "indptr", "indices", "train_idx")}
     if with_feature:
         graph["features"] = _load(path, "features")

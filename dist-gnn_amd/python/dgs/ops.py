@@ -21,6 +21,9 @@ __all__ = [
     "_CAPI_set_random_seed", "_CAPI_set_host_comm", "draw_launch_seeds",
 ]
 
+# host storage registered by _CAPI_tensor_pin_memory: data_ptr -> the tensor.  Holding the
+# tensor keeps its memory alive while registered (a registration outliving its allocation
+# would make HIP reject later copies through memory the allocator reuses).
 _registered = {}
 
 
@@ -129,7 +132,7 @@ def _CAPI_tensor_pin_memory(data):
         return
     p = data.data_ptr()
     check(lib.dgs_host_register(ctypes.c_void_p(p), data.numel() * data.element_size()))
-    _registered[p] = data.numel() * data.element_size()
+    _registered[p] = data
 
 
 def _CAPI_tensor_unpin_memory(data):

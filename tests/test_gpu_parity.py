@@ -370,3 +370,21 @@ def test_rmat_biased_multihop_bit_exact(dgs, fan_out, replace):
         assert np.array_equal(gf.cpu().numpy(), ef)
         assert np.array_equal(gr.cpu().numpy(), er)
         assert np.array_equal(gc.cpu().numpy(), ec)
+
+
+def test_pinned_tensor_outlives_caller_reference(dgs):
+    """A tensor registered by _CAPI_tensor_pin_memory stays allocated while registered (the
+    caller dropping it must not leave a registration over memory the allocator reuses), and
+    _CAPI_tensor_unpin_memory releases it."""
+    t = torch.arange(1 << 16, dtype=torch.int64)
+    dgs.ops._CAPI_tensor_pin_memory(t)
+    p = t.data_ptr()
+    assert t.is_pinned()
+    del t
+    for _ in range(8):  # host allocations + device round trips that could reuse the range
+        h = torch.randn(1 << 16)
+        assert torch.equal(h.cuda().cpu(), h)
+    kept = dgs.ops._registered[p]
+    assert kept.data_ptr() == p and int(kept[-1]) == (1 << 16) - 1
+    dgs.ops._CAPI_tensor_unpin_memory(kept)
+    assert p not in dgs.ops._registered
