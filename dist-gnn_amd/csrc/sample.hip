@@ -483,26 +483,28 @@ constexpr int kBiasRowsPerBlock = kTileRows / 32;  // one 32-lane half-wave per 
 // candidates, then a bitonic merge with the list (the reference's WarpSelect idea, on 32-lane
 // halves of a wave64).  Once the list is full almost no step has a candidate, so the common
 // cost is one compare and one ballot.
+// Edge indices are row-local and 32-bit (a row holds < 2^31 - 1 edges; Sampler checks), which
+// keeps every compare-exchange at two cross-lane shuffles.
 struct HalfTopK {
   float bk = -__builtin_inff();
-  int64_t bi = INT64_MAX;  // INT64_MAX: empty
+  int32_t bi = INT32_MAX;  // INT32_MAX: empty
   int cnt = 0;
   float thr_k = -__builtin_inff();
-  int64_t thr_i = INT64_MAX;
-  static __device__ __forceinline__ void cas(float &k, int64_t &i, int partner_mask, bool better_here) {
+  int32_t thr_i = INT32_MAX;
+  static __device__ __forceinline__ void cas(float &k, int32_t &i, int partner_mask, bool better_here) {
     const float pk = __shfl_xor(k, partner_mask, 32);
-    const int64_t pi = __shfl_xor(i, partner_mask, 32);
+    const int32_t pi = __shfl_xor(i, partner_mask, 32);
     const bool pb = ares_better(pk, pi, k, i);  // partner's entry is the better one
     if (better_here ? pb : !pb) {
       k = pk;
       i = pi;
     }
   }
-  __device__ __forceinline__ void push(float key_i, int64_t i, bool valid, int64_t k, int l) {
+  __device__ __forceinline__ void push(float key_i, int32_t i, bool valid, int64_t k, int l) {
     const bool cand = valid && ares_better(key_i, i, thr_k, thr_i);
     if (!half_ballot(cand)) return;
     float ck = cand ? key_i : -__builtin_inff();
-    int64_t ci = cand ? i : INT64_MAX;
+    int32_t ci = cand ? i : INT32_MAX;
     // bitonic sort of the candidates, descending
 #pragma unroll
     for (int size = 2; size <= 32; size <<= 1) {
@@ -516,14 +518,14 @@ struct HalfTopK {
     // top 32 of list + candidates: pairwise best against the reversed candidates (bitonic),
     // then a descending bitonic merge
     const float rk = __shfl(ck, 31 - l, 32);
-    const int64_t ri = __shfl(ci, 31 - l, 32);
+    const int32_t ri = __shfl(ci, 31 - l, 32);
     if (ares_better(rk, ri, bk, bi)) {
       bk = rk;
       bi = ri;
     }
 #pragma unroll
     for (int stride = 16; stride > 0; stride >>= 1) cas(bk, bi, stride, (l & stride) == 0);
-    cnt = __builtin_popcount(half_ballot(l < k && bi != INT64_MAX));
+    cnt = __builtin_popcount(half_ballot(l < k && bi != INT32_MAX));
     thr_k = __shfl(bk, (int)(k - 1), 32);
     thr_i = __shfl(bi, (int)(k - 1), 32);
   }
@@ -539,7 +541,7 @@ struct HalfTopK {
 // for every step with one.
 struct AresPending {
   float u0 = 0.0f, p0 = 0.0f, u1 = 0.0f, p1 = 0.0f;
-  int64_t i0 = 0, i1 = 0;
+  int32_t i0 = 0, i1 = 0;
   bool h0 = false, h1 = false;
   __device__ __forceinline__ void flush(HalfTopK &top, int64_t k, int l) {
     if (half_ballot(h0)) top.push(h0 ? ares_key(u0, p0) : -__builtin_inff(), i0, h0, k, l);
@@ -555,12 +557,12 @@ struct AresPending {
       if (!h0) {
         u0 = u;
         p0 = p;
-        i0 = i;
+        i0 = (int32_t)i;
         h0 = true;
       } else {
         u1 = u;
         p1 = p;
-        i1 = i;
+        i1 = (int32_t)i;
         h1 = true;
       }
     }
@@ -788,17 +790,21 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
     const int64_t slot = wk + hh;
     if (l < top.cnt) {
       a.ckey[slot * k + l] = top.bk;
-      a.cidx[slot * k + l] = (int32_t)top.bi;
+      a.cidx[slot * k + l] = top.bi;
     }
     if (l == 0) a.ccnt[slot] = top.cnt;
   };
   load_row(h);
   constexpr int kT = kBiasChunk / 32;
+  // the last Philox block of a chunk is the first of the row's next chunk (draws run on)
+  uint32_t carry[4] = {0u, 0u, 0u, 0u};
+  int64_t carry_cb = -1;
   for (int64_t c = c0; c < c1; ++c) {
     while (c >= hnext) {
       flush(h);
       ++h;
       load_row(h);
+      carry_cb = -1;
     }
     const int64_t q = c - hstart;
     if (l == 0 && c == hstart) a.wfirst[h] = (int32_t)wk;
@@ -810,15 +816,26 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
       const int64_t i = i0 + 32 * t;
       p[t] = pr[i < deg ? i : deg - 1];
     }
-    // this lane's 16 draws j = jb + 16q + t lie in 5 consecutive Philox blocks: compute all
-    // five (uniform control flow -- lanes' chain offsets differ, a lazy per-lane refill would
-    // diverge into a Philox per step) and select draw t as word off + t
+    // this lane's 16 draws j = jb + 16q + t lie in 5 consecutive Philox blocks (uniform
+    // control flow -- lanes' chain offsets differ, a lazy per-lane refill would diverge into a
+    // Philox per step); select draw t as word off + t.  The first block was the previous
+    // chunk's last whenever the worker stays in the row, so 4 are computed.
     const int64_t j0 = jb + q * kT;
     const int64_t cb = j0 >> 2;
     const int off = (int)(j0 & 3);
     uint32_t wv[4 * (kT / 4 + 1)];
+    if (cb == carry_cb) {
 #pragma unroll
-    for (int bq = 0; bq < kT / 4 + 1; ++bq) {
+      for (int e = 0; e < 4; ++e) wv[e] = carry[e];
+    } else {
+      const uint4 o = philox4x32_10(make_uint4((uint32_t)cb, (uint32_t)((uint64_t)cb >> 32), sub, 0u), kk);
+      wv[0] = o.x;
+      wv[1] = o.y;
+      wv[2] = o.z;
+      wv[3] = o.w;
+    }
+#pragma unroll
+    for (int bq = 1; bq < kT / 4 + 1; ++bq) {
       const uint64_t cq = (uint64_t)(cb + bq);
       const uint4 o = philox4x32_10(make_uint4((uint32_t)cq, (uint32_t)(cq >> 32), sub, 0u), kk);
       wv[4 * bq + 0] = o.x;
@@ -826,6 +843,9 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
       wv[4 * bq + 2] = o.z;
       wv[4 * bq + 3] = o.w;
     }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) carry[e] = wv[4 * (kT / 4) + e];
+    carry_cb = cb + kT / 4;
 #pragma unroll
     for (int t = 0; t < kT; ++t) {
       const int64_t i = i0 + 32 * t;
@@ -844,7 +864,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
 // slots, then half-wave 0 merges the 8 partial lists and emits the picks.
 __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
   __shared__ float s_key[8][32];
-  __shared__ int64_t s_idx[8][32];
+  __shared__ int32_t s_idx[8][32];
   __shared__ int s_cnt[8];
   const int64_t S = a.Sc.get();
   const uint64_t packed = (uint64_t)*a.hub.count;
@@ -867,7 +887,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
       const int n = have ? a.ccnt[slot] : 0;
       const bool valid = e < n;
       float key_i = -__builtin_inff();
-      int64_t i = INT64_MAX;
+      int32_t i = INT32_MAX;
       if (valid) {
         key_i = a.ckey[slot * k + e];
         i = a.cidx[slot * k + e];

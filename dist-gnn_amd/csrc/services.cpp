@@ -100,6 +100,14 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
   DGS_CHECK(device_id == rank_ || c.host_mode() || !c.initialized(),
             "device_id must equal the communicator rank (sampler.cc:72)");
   DGS_CHECK(num_nodes >= 0 && num_edges >= 0 && n_cache >= 0, "negative sizes");
+  // the biased top-k keeps row-local edge indices in 32 bits
+  if (num_edges >= INT32_MAX) {
+    int64_t prev = indptr[0];
+    for (int64_t v = 1; v <= num_nodes; ++v) {
+      DGS_CHECK(indptr[v] - prev < INT32_MAX, "a row has 2^31 - 1 or more edges");
+      prev = indptr[v];
+    }
+  }
   num_nodes_ = num_nodes;
   num_edges_ = num_edges;
   bias_ = probs != nullptr;
