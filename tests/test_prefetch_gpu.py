@@ -46,10 +46,10 @@ def _batches(n, nb=12, bsz=64, id_dtype=torch.int64):
     return [b.to(id_dtype).cuda() for b in out]
 
 
-def _sequential(dgs, sampler, server, labels, batches, fan_out):
+def _sequential(dgs, sampler, server, labels, batches, fan_out, replace=False):
     out = []
     for s in batches:
-        blocks = sampler._CAPI_sample_node_classifiction(s, fan_out, False)
+        blocks = sampler._CAPI_sample_node_classifiction(s, fan_out, replace)
         x = server._CAPI_get_feature(blocks[-1][1])
         y = dgs.ops._CAPI_cuda_index_select(labels, s)
         out.append((blocks, x, y))
@@ -79,6 +79,22 @@ def test_prefetch_matches_sequential(dgs, depth, bias):
                               depth=depth))
     torch.cuda.synchronize()
     assert len(got) == len(exp)
+    for g, e in zip(got, exp):
+        _same(g, e)
+
+
+@pytest.mark.parametrize("bias", [False, True])
+def test_prefetch_with_replacement(dgs, bias):
+    from DistGNN.dataloading import PrefetchLoader
+    _, sampler, server, labels, _ = _services(dgs, bias)
+    fan_out = [6, 4, 3]
+    batches = _batches(labels.numel(), nb=7)
+    dgs.ops._CAPI_set_random_seed(31)
+    exp = _sequential(dgs, sampler, server, labels, batches, fan_out, replace=True)
+    dgs.ops._CAPI_set_random_seed(31)
+    got = list(PrefetchLoader(sampler, batches, fan_out, replace=True, server=server,
+                              labels=labels, depth=3))
+    torch.cuda.synchronize()
     for g, e in zip(got, exp):
         _same(g, e)
 
