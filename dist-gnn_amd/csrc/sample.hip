@@ -78,17 +78,29 @@ constexpr int kHubShift = 40;
 constexpr uint64_t kHubChunkMask = (uint64_t(1) << kHubShift) - 1;
 constexpr int64_t kHubMaxRows = int64_t(1) << 23;  // hub index field: 24 bits
 struct HubView {
-  int64_t *count, *row, *cptr, *hubid;
+  // thr[h] (biased hubs): the best k-th A-Res key any worker of hub h has published, in the
+  // order-preserving integer form of key_order()
+  int64_t *count, *row, *cptr, *hubid, *thr;
   __host__ __device__ static HubView make(int64_t *base, int64_t S) {
     HubView h;
     h.count = base;
     h.row = base + 8;
     h.cptr = h.row + S;
     h.hubid = h.cptr + S;
+    h.thr = h.hubid + S;
     return h;
   }
-  static size_t bytes(int64_t S) { return sizeof(int64_t) * (size_t)(8 + 3 * S); }
+  static size_t bytes(int64_t S) { return sizeof(int64_t) * (size_t)(8 + 4 * S); }
 };
+
+// float -> int with the same order (negative floats have reversed magnitude bits)
+__device__ __forceinline__ int32_t key_order(float f) {
+  const int32_t i = __float_as_int(f);
+  return i >= 0 ? i : (i ^ 0x7FFFFFFF);
+}
+__device__ __forceinline__ float key_from_order(int32_t m) {
+  return __int_as_float(m >= 0 ? m : (m ^ 0x7FFFFFFF));
+}
 
 // ------------------------------------------------------------------------------------
 // Prep: per-row lookup (one 16-byte node-table load), per-row in-tile output prefix, tile
@@ -149,6 +161,8 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
         a.hub.cptr[h] = (int64_t)(old & kHubChunkMask);
         if (a.use_hubs == 1)
           for (int64_t s2 = 0; s2 < k; ++s2) a.hubslot[i * k + s2] = (int32_t)s2;
+        else
+          a.hub.thr[h] = key_order(-__builtin_inff());
       }
       a.hub.hubid[i] = h;
     }
@@ -548,10 +562,11 @@ struct AresPending {
     if (half_ballot(h1)) top.push(h1 ? ares_key(u1, p1) : -__builtin_inff(), i1, h1, k, l);
     h0 = h1 = false;
   }
-  // edge i (valid) with draw u and weight p
+  // edge i (valid) with draw u and weight p; `filter`: thr is a lower bound of the final k-th
+  // key (the list's own k-th, or a bound another worker of the row published)
   __device__ __forceinline__ void add(float u, float p, int64_t i, bool valid, HalfTopK &top,
-                                      int64_t k, int l) {
-    const bool cand = valid && (!top.filtering(k) || ares_may_pass(u, p, top.thr_k));
+                                      int64_t k, int l, bool filter, float thr) {
+    const bool cand = valid && (!filter || ares_may_pass(u, p, thr));
     if (half_ballot(cand && h0 && h1)) flush(top, k, l);
     if (cand) {
       if (!h0) {
@@ -632,7 +647,7 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
           pv = pr[i];
           ++j;
         }
-        pend.add(u, pv, i, i < deg, top, k, l);
+        pend.add(u, pv, i, i < deg, top, k, l, top.filtering(k), top.thr_k);
       }
       pend.flush(top, k, l);
       if (l < k) {
@@ -768,6 +783,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
   int64_t h = lo;
   int64_t hstart = 0, hnext = 0, deg = 0, jb = 0;
   const float *pr = nullptr;
+  int32_t published = key_order(-__builtin_inff());
   uint2 kk;
   uint32_t sub = 0;
   HalfTopK top;
@@ -783,6 +799,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
     sub = (uint32_t)(32 * ((r % 16) & 3) + l);
     jb = chain_draws(a.rowinfo, r, k, l);
     top = HalfTopK();
+    published = key_order(-__builtin_inff());
   };
   AresPending pend;
   auto flush = [&](int64_t hh) {
@@ -796,6 +813,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
   };
   load_row(h);
   constexpr int kT = kBiasChunk / 32;
+  const int32_t published_none = key_order(-__builtin_inff());
   // the last Philox block of a chunk is the first of the row's next chunk (draws run on)
   uint32_t carry[4] = {0u, 0u, 0u, 0u};
   int64_t carry_cb = -1;
@@ -809,6 +827,10 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
     const int64_t q = c - hstart;
     if (l == 0 && c == hstart) a.wfirst[h] = (int32_t)wk;
     if (l == 0 && c == hnext - 1) a.wlast[h] = (int32_t)wk;
+    // Every worker's k-th key bounds the row's final k-th key from below, so the best one
+    // published so far filters this worker's edges too (stale reads only filter less).
+    const int32_t shared_ord =
+        (int32_t)__hip_atomic_load(a.hub.thr + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int64_t i0 = q * kBiasChunk + l;
     float p[kT];
 #pragma unroll
@@ -854,7 +876,18 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
       x = off == 2 ? wv[t + 2] : x;
       x = off == 3 ? wv[t + 3] : x;
       const float u = curand_uniform_from(x);
-      pend.add(u, p[t], i, i < deg, top, k, l);
+      const bool own = top.filtering(k);
+      const int32_t ord = own ? max(key_order(top.thr_k), shared_ord) : shared_ord;
+      pend.add(u, p[t], i, i < deg, top, k, l, own || shared_ord != published_none,
+               key_from_order(ord));
+    }
+    // publish this worker's k-th key when it improved on what it last published
+    if (top.filtering(k)) {
+      const int32_t mine = key_order(top.thr_k);
+      if (mine > published && mine > shared_ord) {
+        if (l == 0) atomicMax((long long *)(a.hub.thr + h), (long long)mine);
+        published = mine;
+      }
     }
   }
   flush(h);
