@@ -18,6 +18,7 @@
 //     RNG chain is recomputed from the degrees of the chain's earlier rows.
 // Offsets come from a reduce-then-scan over 256-row tiles (no host sync inside the hop).
 #include "dgs_block.cuh"
+#include "dgs_mod.cuh"
 #include "dgs_ops.h"
 #include "dgs_table.cuh"
 
@@ -31,9 +32,20 @@ constexpr int kHubT = 128;       // reservoir tail length above which a row goes
 constexpr int kBiasHubT = 1024;  // biased rows above this degree are split across half-waves
 constexpr int kBiasChunk = 512;  // edges per biased hub chunk (32 lanes x 16 draws)
 constexpr int kBiasHubBlocks = 1024;  // workgroups of the biased hub kernel (8 half-waves each)
-constexpr int kHubBlocks = 2048; // workgroups of the hub kernel (8 waves per SIMD)
+constexpr int kHubBlocks = 1536; // workgroups of the hub kernel: 6 of 8 waves per SIMD, so the
+                                 // other batches in flight (feature gather) find free slots
 constexpr int kMaxPicksLds = 512;
 constexpr int kScanThreads = 1024;
+
+// Workgroups of the uniform hub kernel; DGS_HUB_BLOCKS overrides (occupancy experiments).
+int hub_blocks() {
+  static const int n = [] {
+    const char *e = getenv("DGS_HUB_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : kHubBlocks;
+  }();
+  return n;
+}
 
 using RowInfo = NodeEntry;  // {absolute neighbour-id pointer, degree | location << 56}
 
@@ -211,20 +223,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_hop(const int64_t *bsum,
   }
 }
 
-// x mod d, exact for 2^12 <= d < 2^30.  x/d < 2^20, and the fp32 estimate x * rcp(d) carries a
-// relative error <= 2^-22 (x and d conversions 2^-24 each, v_rcp_f32 1 ulp), i.e. <= 0.25
-// absolute; the fma's own rounding adds <= 2^-4.  Biased by -0.5, the estimate lies in
-// [x/d - 0.8125, x/d - 0.1875], so its truncation q is floor(x/d) or one less: r = x - q*d is
-// in [0, 2d) and one conditional subtract finishes (the generic % spends four quarter-rate
-// multiplies).  tools/modfuzz.hip: every x for ~1K divisors + 2^34 random pairs, 0 mismatches.
-constexpr uint32_t kModBigMin = 4096;
-__device__ __forceinline__ uint32_t mod_big(uint32_t x, uint32_t d) {
-  const float rcp = __builtin_amdgcn_rcpf((float)d);
-  const uint32_t q = (uint32_t)(int32_t)__builtin_fmaf((float)x, rcp, -0.5f);
-  const uint32_t r = x - q * d;
-  return r >= d ? r - d : r;
-}
-
 // ------------------------------------------------------------------------------------
 // Uniform sampling (rowwise_sampling.cu K2/K3).  Arguments shared by the kernels below.
 struct UniformArgs {
@@ -251,6 +249,27 @@ __device__ __forceinline__ void emit_slots(const UniformArgs &a, int64_t S, int6
     a.rowpos[out + s2] = r;
     a.col[out + s2] = v;
     table_record(a.table, v, S + out + s2);
+  }
+}
+
+// The 8 draws of one lane in one 512-edge hub chunk (idx = k + 512 q + lane + 64 tt + 128 w)
+// with 32-bit indices: every idx of the chunk is below 2^30.
+template <typename Mod>
+__device__ __forceinline__ void hub_chunk32(const uint4 &o4a, const uint4 &o4b, int64_t q,
+                                            int64_t k, int64_t deg, int lane, int32_t *sl,
+                                            Mod mod) {
+  const uint32_t b0 = (uint32_t)(k + 512 * q) + (uint32_t)lane;
+  const uint32_t deg32 = (uint32_t)deg, k32 = (uint32_t)k;
+  const bool full = k + 512 * q + 512 <= deg;
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const uint4 o4 = tt ? o4b : o4a;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t idx = b0 + 64u * tt + 128u * w;
+      const uint32_t num = mod(u4_get(o4, w), idx + 1u);
+      if (num < k32 && (full || idx < deg32)) atomicMax(sl + num, (int32_t)idx);
+    }
   }
 }
 
@@ -296,24 +315,19 @@ __device__ __forceinline__ void hub_reservoir(const UniformArgs &a, int64_t gw, 
         make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)lane, 0u), kk);
     const uint4 o4b = philox4x32_10(
         make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)(lane + 64), 0u), kk);
-    // every d = idx + 1 of this chunk is >= k + 512 q + 1 (wave-uniform test)
-    if (k + 512 * q + 1 >= (int64_t)kModBigMin && deg < (int64_t(1) << 30)) {
-      // 32-bit and branch-free up to the (rare) hit; a chunk entirely inside the row skips the
-      // bound test
-      const uint32_t b0 = (uint32_t)(k + 512 * q) + (uint32_t)lane;
-      const uint32_t deg32 = (uint32_t)deg, k32 = (uint32_t)k;
-      const bool full = k + 512 * q + 512 <= deg;
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const uint4 o4 = tt ? o4b : o4a;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const uint32_t idx = b0 + 64u * tt + 128u * w;
-          const uint32_t num = mod_big(u4_get(o4, w), idx + 1u);
-          if (num < k32 && (full || idx < deg32)) atomicMax(sl + num, (int32_t)idx);
-        }
-      }
-    } else {
+    // every d = idx + 1 of this chunk lies in [k + 512 q + 1, k + 512 q + 512]: the modulo
+    // is chosen per chunk (wave-uniform test); the 32-bit forms are branch-free up to the (rare)
+    // hit, and a chunk entirely inside the row skips the bound test
+    const int64_t dmin = k + 512 * q + 1;
+    if (dmin >= (int64_t)kModBigMin && deg < (int64_t(1) << 24))
+      hub_chunk32(o4a, o4b, q, k, deg, lane, sl, mod_big<true>);
+    else if (dmin >= (int64_t)kModBigMin && deg < (int64_t(1) << 30))
+      hub_chunk32(o4a, o4b, q, k, deg, lane, sl, mod_big<false>);
+    else if (dmin + 511 <= (int64_t)kModMidMax && dmin >= 257)
+      hub_chunk32(o4a, o4b, q, k, deg, lane, sl, mod_mid<true>);
+    else if (dmin + 511 <= (int64_t)kModMidMax)
+      hub_chunk32(o4a, o4b, q, k, deg, lane, sl, mod_mid<false>);
+    else {
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
         const uint4 o4 = tt ? o4b : o4a;
@@ -392,7 +406,9 @@ __device__ __forceinline__ void sample_rows(const UniformArgs &a, int64_t blk, i
       for (int w = 0; w < 4; ++w) {
         const int64_t idx = base + 128 * w;
         if (idx < deg) {
-          const uint32_t num = u4_get(o4, w) % (uint32_t)(idx + 1);
+          // every row here has deg <= k + 128 when hubs are on (group-uniform test)
+          const uint32_t x = u4_get(o4, w), d = (uint32_t)(idx + 1);
+          const uint32_t num = deg <= (int64_t)kModMidMax ? mod_mid<false>(x, d) : x % d;
           if ((int64_t)num < k) atomicMax(sl + num, (int32_t)idx);
         }
       }
@@ -417,8 +433,12 @@ __global__ __launch_bounds__(256) void k_hub_reservoir(UniformArgs a, const int6
       *d_nnz = tot;
     }
   }
-  hub_reservoir(a, ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6,
-                ((int64_t)gridDim.x * blockDim.x) >> 6);
+  // the wave index is wave-uniform: chunk bookkeeping and the chunk index (Philox counter
+  // word 0) then live in scalar registers, and so do the first round's M0 * q product and the
+  // second round's M1 product of both Philox blocks of a chunk
+  const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) +
+                     __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  hub_reservoir(a, gw, ((int64_t)gridDim.x * blockDim.x) >> 6);
 }
 
 template <bool kReplace>
@@ -1016,7 +1036,7 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     const size_t lds = replace ? 16 : sizeof(int32_t) * (size_t)kRowsPerBlock * k;
     const int64_t row_blocks = ceil_div(S, kRowsPerBlock);
     if (use_hubs) {
-      hipLaunchKernelGGL(k_hub_reservoir, dim3(kHubBlocks), dim3(256), 0, st, ua,
+      hipLaunchKernelGGL(k_hub_reservoir, dim3(hub_blocks()), dim3(256), 0, st, ua,
                          (const int64_t *)bsum, boff, d_nnz);
       DGS_LAUNCH_CHECK();
     }
