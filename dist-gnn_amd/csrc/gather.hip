@@ -132,8 +132,14 @@ struct StridedSrc {
   }
 };
 
-constexpr int kGatherThreads = 256;
-constexpr int kGatherUnroll = 4;
+#ifndef DGS_GATHER_UNROLL
+#define DGS_GATHER_UNROLL 4
+#endif
+#ifndef DGS_GATHER_THREADS
+#define DGS_GATHER_THREADS 256
+#endif
+constexpr int kGatherThreads = DGS_GATHER_THREADS;
+constexpr int kGatherUnroll = DGS_GATHER_UNROLL;
 
 template <int V, typename Src>
 __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nchunks,
