@@ -182,8 +182,8 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    # only the gather kernel carries events in the timed region (its own start/end stamps, no
-    # marker packets between the measured kernels)
+    # only the gather kernel is measured in the timed region: its workgroups stamp their own
+    # start / end (no stream markers between the measured kernels)
     dgs.ops.profile_enable(dgs.ops.PROFILE_GATHER)
     edges = rows = 0
     t0 = time.perf_counter()
@@ -292,9 +292,10 @@ def main():
             "kernel": ("k_gather<16, StridedSrc> (P2PCacheFeatureServer gather, computed row "
                        "addresses)" if layout >= 0 else
                        "k_gather<16, TableSrc> (P2PCacheFeatureServer gather, address table)"),
-            "timing": ("hipExtLaunchKernelGGL start/stop events (GPU-side kernel start/end) "
-                       "over the timed region, where each gather shares the GPU with the "
-                       "sampling kernels of the other batches in flight"),
+            "timing": ("device-side s_memrealtime stamps per workgroup (first workgroup start to "
+                       "last workgroup end of each launch, 100 MHz wall clock) over the timed "
+                       "region, where each gather shares the GPU with the sampling kernels of the "
+                       "other batches in flight"),
             "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "bytes_per_launch": g_bytes, "avg_launch_ms": g_ms,
@@ -339,6 +340,23 @@ def seed_slice(train, rank, world):
     return train[rank * per:(rank + 1) * per]
 
 
+def host_info():
+    """The box's CPU as the baseline ran on it (state the core count)."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "usable_cpus": usable}
+
+
 def cpu_baseline(indptr, indices, probs, feats, train, fan_out, args):
     """The oracle's OpenMP restatement on the host cores (DGL is not installed): row-wise
     sampling per hop (uniform, or biased when probs is given) + relabel + feature gather, same
@@ -371,8 +389,19 @@ def cpu_baseline(indptr, indices, probs, feats, train, fan_out, args):
         if time.perf_counter() - t0 > args.cpu_baseline_seconds:
             break
     dt = time.perf_counter() - t0
+    # the CPU gather baseline proper is torch.index_select on the host feature
+    # tensor with the same nids (here: the last batch's frontier, repeated for ~1 s)
+    torch.set_num_threads(threads)
+    nid = torch.from_numpy(np.ascontiguousarray(cur))
+    reps, t1 = 0, time.perf_counter()
+    while reps < 3 or time.perf_counter() - t1 < 1.0:
+        torch.index_select(feats, 0, nid)
+        reps += 1
+    ts_gbps = reps * nid.numel() * (2 * args.dim * 4 + 8) / (time.perf_counter() - t1) / 1e9
     return {"value": edges / dt, "unit": "sampled edges/s", "cores": threads, "kind": "port",
+            "host": host_info(),
             "gather_GBps": rows * (2 * args.dim * 4 + 8) / dt / 1e9,
+            "gather_GBps_torch_index_select": ts_gbps,
             "sample": (f"{batches} batches of B={args.batch}, fan-out {fan_out}, same graph; "
                        f"oracle/dgs_oracle.c OpenMP {'biased' if probs is not None else 'uniform'} "
                        f"sampler ({threads} threads) + serial relabel "

@@ -190,6 +190,32 @@ hipEvent_t take_event() {
   DGS_HIP(hipEventCreate(&e));
   return e;
 }
+
+struct StampRec {
+  uint64_t *buf;
+  int64_t nblocks;
+  int which;
+};
+std::vector<StampRec> &stamp_recs() {
+  static std::vector<StampRec> v;
+  return v;
+}
+std::vector<std::pair<int64_t, uint64_t *>> &stamp_pool() {
+  static std::vector<std::pair<int64_t, uint64_t *>> v;
+  return v;
+}
+void add_measure(int which, double ms) {
+  if (which == 0) {
+    profiler().gather_ms += ms;
+    profiler().gather_n += 1;
+  } else if (which == 2) {
+    profiler().select_ms += ms;
+    profiler().select_n += 1;
+  } else {
+    profiler().sample_ms += ms;
+    profiler().sample_n += 1;
+  }
+}
 }  // namespace
 
 Profiler &profiler() {
@@ -205,6 +231,23 @@ KernelEvents profile_kernel(int which) {
   ev.stop = take_event();
   pending().push_back(EvPair{ev.start, ev.stop, which, nullptr});
   return ev;
+}
+
+uint64_t *profile_stamps(int which, int64_t nblocks) {
+  if (!profiler().wants(which) || nblocks <= 0) return nullptr;
+  std::lock_guard<std::mutex> g(prof_mu());
+  uint64_t *buf = nullptr;
+  auto &pool = stamp_pool();
+  for (auto it = pool.begin(); it != pool.end(); ++it) {
+    if (it->first >= nblocks) {
+      buf = it->second;
+      pool.erase(it);
+      break;
+    }
+  }
+  if (!buf) DGS_HIP(hipMalloc(reinterpret_cast<void **>(&buf), sizeof(uint64_t) * 2 * nblocks));
+  stamp_recs().push_back(StampRec{buf, nblocks, which});
+  return buf;
 }
 
 void profile_begin(hipStream_t st, int which) {
@@ -230,6 +273,26 @@ void profile_end(hipStream_t st, int which) {
 
 void profile_collect() {
   std::lock_guard<std::mutex> g(prof_mu());
+  auto &sr = stamp_recs();
+  if (!sr.empty()) {
+    DGS_HIP(hipDeviceSynchronize());
+    int dev = 0, khz = 0;
+    DGS_HIP(hipGetDevice(&dev));
+    DGS_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+    std::vector<uint64_t> h;
+    for (auto &r : sr) {
+      h.resize((size_t)(2 * r.nblocks));
+      DGS_HIP(hipMemcpy(h.data(), r.buf, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost));
+      uint64_t t0 = ~0ull, t1 = 0;
+      for (int64_t b = 0; b < r.nblocks; ++b) {
+        t0 = h[2 * b] < t0 ? h[2 * b] : t0;
+        t1 = h[2 * b + 1] > t1 ? h[2 * b + 1] : t1;
+      }
+      if (t1 > t0 && khz > 0) add_measure(r.which, (double)(t1 - t0) / (double)khz);
+      stamp_pool().push_back({r.nblocks, r.buf});
+    }
+    sr.clear();
+  }
   auto &pv = pending();
   for (auto &ev : pv) {
     if (!ev.b) continue;
@@ -242,16 +305,7 @@ void profile_collect() {
       pool().push_back(ev.b);
       continue;
     }
-    if (ev.which == 0) {
-      profiler().gather_ms += ms;
-      profiler().gather_n += 1;
-    } else if (ev.which == 2) {
-      profiler().select_ms += ms;
-      profiler().select_n += 1;
-    } else {
-      profiler().sample_ms += ms;
-      profiler().sample_n += 1;
-    }
+    add_measure(ev.which, ms);
     pool().push_back(ev.a);
     pool().push_back(ev.b);
   }

@@ -143,6 +143,12 @@ struct KernelEvents {
   hipEvent_t start = nullptr, stop = nullptr;
 };
 KernelEvents profile_kernel(int which);
+// Device-side stamps of one kernel launch: when measurement `which` is on, a device buffer of
+// 2 * nblocks uint64 that the kernel fills with each workgroup's s_memrealtime at its start and
+// after its last store (the launch's duration = last end - first start, the kernel's own
+// execution span); nullptr otherwise.  Unlike stream events it excludes the tail of the
+// previous kernel on the stream and any wait for free CUs before the first workgroup starts.
+uint64_t *profile_stamps(int which, int64_t nblocks);
 // Stream events at both ends of a group of launches (one marker before the first and one
 // after the last kernel; used around a whole sample call, where the stream is idle anyway,
 // never between the kernels being measured).

@@ -144,8 +144,11 @@ constexpr int kGatherUnroll = DGS_GATHER_UNROLL;
 template <int V, typename Src>
 __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nchunks,
                                                            uint32_t cpr, FastDivU32 fd,
-                                                           char *__restrict__ out) {
+                                                           char *__restrict__ out,
+                                                           uint64_t *stamp) {
   using T = typename VecT<V>::T;
+  // profiling only (stamp != nullptr, a kernel argument: uniform branch)
+  if (stamp && threadIdx.x == 0) stamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   const uint32_t base = blockIdx.x * (uint32_t)(kGatherThreads * kGatherUnroll) + threadIdx.x;
   // Branch-free: out-of-range chunks re-read the last chunk and skip only the store, so the
   // U independent id -> address -> row load chains issue back to back (3 waits, not 3U).
@@ -176,6 +179,11 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nch
     // streams past L2 instead of evicting the rows other waves are fetching
     if (g < nchunks) __builtin_nontemporal_store(v[u], reinterpret_cast<T *>(out + (size_t)g * V));
   }
+  if (stamp) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) stamp[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 template <typename Src>
@@ -192,15 +200,15 @@ void launch_gather_v(int V, Src src, int64_t n, int64_t row_bytes, char *out, hi
     const uint32_t nchunks = (uint32_t)(rows * cpr);
     const dim3 grid((unsigned)ceil_div(nchunks, kGatherThreads * kGatherUnroll));
     char *o = out + r0 * row_bytes;
-    const KernelEvents ev = profile_kernel(which);
+    uint64_t *stamp = profile_stamps(which, (int64_t)grid.x);
     const dim3 block(kGatherThreads);
     const uint32_t c32 = (uint32_t)cpr;
     switch (V) {
-      case 16: hipExtLaunchKernelGGL((k_gather<16, Src>), grid, block, 0, st, ev.start, ev.stop, 0, s, nchunks, c32, fd, o); break;
-      case 8: hipExtLaunchKernelGGL((k_gather<8, Src>), grid, block, 0, st, ev.start, ev.stop, 0, s, nchunks, c32, fd, o); break;
-      case 4: hipExtLaunchKernelGGL((k_gather<4, Src>), grid, block, 0, st, ev.start, ev.stop, 0, s, nchunks, c32, fd, o); break;
-      case 2: hipExtLaunchKernelGGL((k_gather<2, Src>), grid, block, 0, st, ev.start, ev.stop, 0, s, nchunks, c32, fd, o); break;
-      default: hipExtLaunchKernelGGL((k_gather<1, Src>), grid, block, 0, st, ev.start, ev.stop, 0, s, nchunks, c32, fd, o); break;
+      case 16: hipLaunchKernelGGL((k_gather<16, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp); break;
+      case 8: hipLaunchKernelGGL((k_gather<8, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp); break;
+      case 4: hipLaunchKernelGGL((k_gather<4, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp); break;
+      case 2: hipLaunchKernelGGL((k_gather<2, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp); break;
+      default: hipLaunchKernelGGL((k_gather<1, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp); break;
     }
     DGS_LAUNCH_CHECK();
   }

@@ -55,6 +55,12 @@ def main():
           f"{busy / span:.1%}, summed kernel time {tot / span:.2f}x the window, "
           f"{len(win)} kernels ({len(win) / a.steps:.1f}/step), {len(gaps)} idle gaps, "
           f"total {sum(gaps) / 1e3:.1f} us, largest {[round(x / 1e3, 1) for x in gaps[-5:]]}")
+    # the feature gather's own launches in the window (what bench.py's roofline.avg_launch_ms
+    # measures with HIP events over the timed region)
+    gw = [e - s for s, e, n in rows if "k_gather<16" in n and "StridedSrc" in n
+          and s >= t0 and e <= t1]
+    if gw:
+        print(f"feature gather in the window: {len(gw)} launches, avg {sum(gw) / len(gw) / 1e3:.2f} us")
     per = {}
     for s, e, n in win:
         k = short_name(n)
