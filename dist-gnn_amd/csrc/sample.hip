@@ -105,6 +105,28 @@ struct HubView {
   static size_t bytes(int64_t S) { return sizeof(int64_t) * (size_t)(8 + 4 * S); }
 };
 
+// Largest h in [0, H) with cptr[h] <= c (cptr nondecreasing, cptr[0] <= c), by a W-ary search:
+// the W lanes of a wave (W = 64) or half-wave (W = 32, c uniform per half) probe W evenly
+// spaced entries per round, so a hub list of H rows costs ceil(log_W H) dependent loads instead
+// of log2 H (one round for H <= W, two for H <= W^2).  Every lane of the group must be active.
+template <int W>
+__device__ __forceinline__ int64_t group_search(const int64_t *cptr, int64_t H, int64_t c) {
+  const int lane = threadIdx.x & (W - 1);
+  int64_t lo = 0, n = H;  // answer in [lo, lo + n)
+  while (n > 1) {
+    const int64_t step = (n + W - 1) / W;
+    const int64_t idx = lo + (int64_t)lane * step;
+    const bool ok = lane == 0 || (idx < lo + n && cptr[idx] <= c);
+    const uint64_t b = __ballot(ok);
+    const uint64_t mine = W == 64 ? b : ((threadIdx.x & 32) ? (b >> 32) : (b & 0xFFFFFFFFull));
+    const int cnt = __popcll(mine);  // nondecreasing probes: the ok lanes are a prefix
+    const int64_t end = lo + n;
+    lo += (int64_t)(cnt - 1) * step;
+    n = end - lo < step ? end - lo : step;
+  }
+  return lo;
+}
+
 // float -> int with the same order (negative floats have reversed magnitude bits)
 __device__ __forceinline__ int32_t key_order(float f) {
   const int32_t i = __float_as_int(f);
@@ -290,12 +312,7 @@ __device__ __forceinline__ void hub_reservoir(const UniformArgs &a, int64_t gw, 
   // chunk would dominate the Philox work).
   const int64_t c0 = total * gw / nwaves, c1 = total * (gw + 1) / nwaves;
   if (c0 >= c1) return;
-  int64_t lo = 0, hi = H;  // largest h with cptr[h] <= c0
-  while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (hub.cptr[mid] <= c0) lo = mid; else hi = mid;
-  }
-  int64_t h = lo;
+  int64_t h = group_search<64>(hub.cptr, H, c0);  // largest h with cptr[h] <= c0
   int64_t hstart = hub.cptr[h], hnext = h + 1 < H ? hub.cptr[h + 1] : total;
   int64_t r = hub.row[h];
   int64_t deg = ri_deg(a.rowinfo[r]);
@@ -795,12 +812,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
   const int64_t c1 = bias_worker_c0(total, wk + 1, nw);
   if (c0 >= c1) return;
   const int64_t k = a.k;
-  int64_t lo = 0, hi = H;  // largest h with cptr[h] <= c0
-  while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (a.hub.cptr[mid] <= c0) lo = mid; else hi = mid;
-  }
-  int64_t h = lo;
+  int64_t h = group_search<32>(a.hub.cptr, H, c0);  // largest h with cptr[h] <= c0
   int64_t hstart = 0, hnext = 0, deg = 0, jb = 0;
   const float *pr = nullptr;
   int32_t published = key_order(-__builtin_inff());
