@@ -41,8 +41,8 @@ def log(*a):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=100)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--warmup", type=int, default=30)
     p.add_argument("--batch", type=int, default=1024)
     p.add_argument("--fan-out", type=str, default="15,10,5")
     p.add_argument("--scale", type=int, default=21)   # products-like: 2,097,152 nodes
@@ -188,7 +188,9 @@ def main():
     edges = rows = 0
     t0 = time.perf_counter()
     last_nids = []
+    step_t = []
     for blocks, x, _ in it:
+        step_t.append(time.perf_counter())
         edges += sum(b[2].numel() for b in blocks)
         rows += x.shape[0]
         if len(last_nids) < 20:
@@ -199,6 +201,10 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     prof = dgs.ops.profile_read()
+    # host-side spacing of consecutive batches handed out by the loader (jitter diagnostics)
+    gaps = np.diff(np.array([t0] + step_t)) * 1e3
+    step_gaps = {"p10": float(np.percentile(gaps, 10)), "p50": float(np.median(gaps)),
+                 "p90": float(np.percentile(gaps, 90)), "max": float(gaps.max())}
     host_rows = sum(float((~cached_mask[n.long()]).sum()) / max(n.numel(), 1)
                     for n in last_nids) / max(len(last_nids), 1)
     # informational, outside the timed region: the sequential loop's latency per sample call
@@ -275,6 +281,7 @@ def main():
             "cache_frac": args.cache_frac,
             "pipeline_depth": args.depth,
         },
+        "host_step_gap_ms": step_gaps,
         "host_row_share": host_rows,
         # host rows cross PCIe Gen5 x16 (63 GB/s spec): their read rate during the gather
         "gather_host_read_GBps": (host_rows * rows * row_bytes / (prof["gather_ms"] * 1e-3) / 1e9

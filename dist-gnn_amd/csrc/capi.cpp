@@ -401,6 +401,7 @@ int dgs_profile_enable(int mask) {
     if (mask != 0 && (mask & ~7) != 0) m = 7;
     profiler().mask = m;
     profiler().on = m != 0;
+    if (m & 5) profile_reserve();  // gather or select stamps
   });
 }
 

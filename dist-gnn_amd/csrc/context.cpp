@@ -195,7 +195,20 @@ struct StampRec {
   uint64_t *buf;
   int64_t nblocks;
   int which;
+  bool own;  // a separate allocation (slab full), returned to the pool at collect
 };
+// Workgroup stamps are bump-allocated from one slab reserved when profiling is switched on,
+// so a profiled launch inside a timed region never calls hipMalloc.  256 MB holds 2 x 8 B
+// for 16 M workgroups (B = 1024: ~5000 gathers; B = 8192: ~600) before falling back.
+constexpr int64_t kStampSlabWords = int64_t(32) << 20;
+struct StampSlab {
+  uint64_t *base = nullptr;
+  int64_t used = 0;
+};
+StampSlab &stamp_slab() {
+  static StampSlab s;
+  return s;
+}
 std::vector<StampRec> &stamp_recs() {
   static std::vector<StampRec> v;
   return v;
@@ -237,6 +250,13 @@ uint64_t *profile_stamps(int which, int64_t nblocks) {
   if (!profiler().wants(which) || nblocks <= 0) return nullptr;
   std::lock_guard<std::mutex> g(prof_mu());
   uint64_t *buf = nullptr;
+  StampSlab &slab = stamp_slab();
+  if (slab.base && slab.used + 2 * nblocks <= kStampSlabWords) {
+    buf = slab.base + slab.used;
+    slab.used += 2 * nblocks;
+    stamp_recs().push_back(StampRec{buf, nblocks, which, false});
+    return buf;
+  }
   auto &pool = stamp_pool();
   for (auto it = pool.begin(); it != pool.end(); ++it) {
     if (it->first >= nblocks) {
@@ -246,7 +266,7 @@ uint64_t *profile_stamps(int which, int64_t nblocks) {
     }
   }
   if (!buf) DGS_HIP(hipMalloc(reinterpret_cast<void **>(&buf), sizeof(uint64_t) * 2 * nblocks));
-  stamp_recs().push_back(StampRec{buf, nblocks, which});
+  stamp_recs().push_back(StampRec{buf, nblocks, which, true});
   return buf;
 }
 
@@ -271,6 +291,13 @@ void profile_end(hipStream_t st, int which) {
   }
 }
 
+void profile_reserve() {
+  std::lock_guard<std::mutex> g(prof_mu());
+  StampSlab &slab = stamp_slab();
+  if (!slab.base)
+    DGS_HIP(hipMalloc(reinterpret_cast<void **>(&slab.base), sizeof(uint64_t) * kStampSlabWords));
+}
+
 void profile_collect() {
   std::lock_guard<std::mutex> g(prof_mu());
   auto &sr = stamp_recs();
@@ -289,9 +316,10 @@ void profile_collect() {
         t1 = h[2 * b + 1] > t1 ? h[2 * b + 1] : t1;
       }
       if (t1 > t0 && khz > 0) add_measure(r.which, (double)(t1 - t0) / (double)khz);
-      stamp_pool().push_back({r.nblocks, r.buf});
+      if (r.own) stamp_pool().push_back({r.nblocks, r.buf});
     }
     sr.clear();
+    stamp_slab().used = 0;
   }
   auto &pv = pending();
   for (auto &ev : pv) {

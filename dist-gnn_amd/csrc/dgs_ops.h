@@ -155,6 +155,8 @@ uint64_t *profile_stamps(int which, int64_t nblocks);
 void profile_begin(hipStream_t st, int which);
 void profile_end(hipStream_t st, int which);
 void profile_collect();
+// reserves the workgroup-stamp slab (called when gather profiling is switched on)
+void profile_reserve();
 // cache-map helpers: tab[v] = (loc << 56) | row
 void loctab_init_host(int64_t *tab, int64_t n, hipStream_t st);
 void loctab_assign(int64_t *tab, const int64_t *nids, int64_t n, int loc, hipStream_t st);

@@ -9,6 +9,7 @@ waits for the current one.  One thread, one sampler and one feature server: the 
 sampling context per stream over the shared graph.
 """
 import collections
+import os
 import threading
 
 import torch
@@ -21,6 +22,8 @@ __all__ = ["PrefetchLoader"]
 # (scratch, relabel tables: 16 B per node) per stream for its lifetime, and a context's first
 # use allocates it.
 _STREAMS = {}
+# DGS_PREFETCH_SYNC=1: issue each batch's launches on the caller's thread (experiments)
+_HOST_ASYNC = os.environ.get("DGS_PREFETCH_SYNC", "0") != "1"
 _STREAMS_LOCK = threading.Lock()
 
 
@@ -88,7 +91,7 @@ class PrefetchLoader:
             # the stream is not touched again before result(): the sampler's launcher thread
             # may issue the launches
             pending = self.sampler._sample_begin(seeds, self.fan_out, self.replace,
-                                                 launch_seeds, host_async=True)
+                                                 launch_seeds, host_async=_HOST_ASYNC)
         self._inflight.append((pending, y, st))
 
     def __iter__(self):
