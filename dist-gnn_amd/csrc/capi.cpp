@@ -152,6 +152,25 @@ int dgs_index_select(const void *data, int64_t row_bytes, const void *nid, int n
   });
 }
 
+int dgs_index_select_device(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
+                            int64_t n, void *out, void *stream) {
+  return guard([&] { gather_plain(data, row_bytes, nid, nid_bytes, n, out, S(stream)); });
+}
+
+int dgs_stream_wait(void *producer, void *consumer) {
+  return guard([&] {
+    // one event per calling thread: a wait already enqueued keeps the record it saw, so the
+    // event can be recorded again at once
+    thread_local hipEvent_t ev = [] {
+      hipEvent_t e;
+      DGS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      return e;
+    }();
+    DGS_HIP(hipEventRecord(ev, S(producer)));
+    DGS_HIP(hipStreamWaitEvent(S(consumer), ev, 0));
+  });
+}
+
 int dgs_sample_neighbors(const int64_t *seeds, int64_t Sn, const int64_t *indptr,
                          const int64_t *indices, const float *probs, int64_t num_picks,
                          int replace, int64_t *out_row, int64_t *out_col, int64_t *nnz_out,

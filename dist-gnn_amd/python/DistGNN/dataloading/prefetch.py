@@ -15,6 +15,7 @@ import threading
 import torch
 
 import dgs
+from dgs._lib import _raw_stream
 
 __all__ = ["PrefetchLoader"]
 
@@ -54,91 +55,105 @@ class PrefetchLoader:
                  depth=2, device=None):
         if depth < 1:
             raise ValueError("depth must be >= 1")
-        self.sampler, self.server, self.labels = sampler, server, labels
-        self.fan_out, self.replace = list(fan_out), bool(replace)
         self.device = torch.device(device) if device is not None else \
             torch.device("cuda", torch.cuda.current_device())
+        if labels is not None:
+            if labels.dtype not in (torch.int32, torch.int64, torch.float32):
+                raise RuntimeError("Value can only be int32 or int64 or float32")
+            # the per-batch label gather reads device memory (host labels are copied once)
+            labels = labels.to(self.device).contiguous()
+        self.sampler, self.server, self.labels = sampler, server, labels
+        self.fan_out, self.replace = list(fan_out), bool(replace)
         self._seeds = iter(seeds_iter)
         self._exhausted = False
         self._streams = _worker_streams(self.device, depth)
-        # reusable cross-stream events: caller -> batch stream, batch stream -> caller (one
-        # gather stream per batch stream: more streams than the process's hardware queues
-        # would serialise them)
-        self._ev_submit = [torch.cuda.Event() for _ in range(depth)]
-        self._ev_done = torch.cuda.Event()
+        self._st = [s.cuda_stream for s in self._streams]
+        self._dev = self.device.index
         self._inflight = collections.deque()
         self._n = 0
 
+    def _caller_stream(self):
+        if _raw_stream is not None:
+            return _raw_stream(self._dev)
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    # Stream ordering (no record_stream on the outputs): every output is allocated on the
+    # caller's stream C and then written on the batch stream B only after B waits for C
+    # (dgs.ops._stream_wait, recorded after the allocations, so C's earlier users of the
+    # memory are done); C waits for B before the outputs are handed out or dropped.
     def _submit(self):
         try:
             seeds = next(self._seeds)
         except StopIteration:
             self._exhausted = True
             return
-        w = self._n % len(self._streams)
-        st = self._streams[w]
+        w = self._n % len(self._st)
+        st = self._st[w]
         self._n += 1
-        # the seeds (and any memory the caller's stream recycled) come from the caller's stream
-        ev = self._ev_submit[w]
-        ev.record(torch.cuda.current_stream(self.device))
-        st.wait_event(ev)
-        seeds.record_stream(st)
+        cur = self._caller_stream()
+        # the caller may drop its seeds at once: their memory must outlive B's reads
+        seeds.record_stream(self._streams[w])
         launch_seeds = dgs.ops.draw_launch_seeds(len(self.fan_out))
-        with torch.cuda.stream(st):
-            y = None
-            if self.labels is not None:  # depends on the seeds only: issued first
-                y = dgs.ops._CAPI_cuda_index_select(self.labels, seeds)
-            # the stream is not touched again before result(): the sampler's launcher thread
-            # may issue the launches
-            pending = self.sampler._sample_begin(seeds, self.fan_out, self.replace,
-                                                 launch_seeds, host_async=_HOST_ASYNC)
-        self._inflight.append((pending, y, st))
+        prep = self.sampler._prepare(seeds, self.fan_out)  # int64 seeds + outputs, on C
+        s64 = prep[0]
+        y = None
+        if self.labels is not None:
+            y = torch.empty((s64.numel(),) + tuple(self.labels.shape[1:]),
+                            dtype=self.labels.dtype, device=self.device)
+        dgs.ops._stream_wait(cur, st)
+        if y is not None:  # depends on the seeds only: issued first
+            dgs.ops._index_select_into(self.labels, s64, y, st)
+        # B is not touched again before result(): the sampler's launcher thread may issue
+        # the launches
+        pending = self.sampler._begin_prepared(seeds, prep, self.replace, launch_seeds,
+                                               _HOST_ASYNC, st)
+        self._inflight.append((pending, y, w))
 
     def __iter__(self):
         return self
 
     def __next__(self):
-        while not self._exhausted and len(self._inflight) < len(self._streams):
+        while not self._exhausted and len(self._inflight) < len(self._st):
             self._submit()
         if not self._inflight:
             raise StopIteration
-        pending, y, st = self._inflight.popleft()
+        pending, y, w = self._inflight.popleft()
+        st = self._st[w]
+        cur = self._caller_stream()
         try:
-            with torch.cuda.stream(st):
-                blocks = pending.result()
+            blocks = pending.result(cast=False)
         except BaseException:
+            dgs.ops._stream_wait(st, cur)
             self.close()
             raise
         x = None
         if self.server is not None:
-            with torch.cuda.stream(st):
-                x = self.server._CAPI_get_feature(blocks[-1][1])
-        cur = torch.cuda.current_stream(self.device)
-        self._ev_done.record(st)
-        cur.wait_event(self._ev_done)
-        # the caller's stream now uses memory allocated on the batch's streams: with int64 ids
-        # every block tensor but the caller's seeds is a view of one buffer
-        if blocks[-1][1].dtype == torch.int64:
-            blocks[-1][1].record_stream(cur)
-        else:
-            for b in blocks:
-                for t in b[1:]:
-                    t.record_stream(cur)
-        for t in (x, y):
-            if t is not None:
-                t.record_stream(cur)
+            front = blocks[-1][1]
+            x = self.server._get_feature_alloc(front)
+            dgs.ops._stream_wait(cur, st)
+            self.server._get_feature_into(front, x, st)
+        dgs.ops._stream_wait(st, cur)
+        dt = self.sampler._id_dtype
+        if dt != torch.int64:  # int32 graphs: cast on the caller's stream, now ordered after B
+            cast, cur_seeds = [], blocks[0][0]
+            for _, fr, r, c in blocks:
+                fr, r, c = fr.to(dt), r.to(dt), c.to(dt)
+                cast.append((cur_seeds, fr, r, c))
+                cur_seeds = fr
+            blocks = cast
         return blocks, x, y
 
     def close(self):
         """Ends the calls still in flight (a stream takes a new call only after its last one
-        has ended); their results are dropped."""
+        has ended); their results are dropped once the caller's stream is ordered after them."""
+        cur = self._caller_stream() if self._inflight else None
         while self._inflight:
-            pending, _, st = self._inflight.popleft()
+            pending, _, w = self._inflight.popleft()
             try:
-                with torch.cuda.stream(st):
-                    pending.result()
+                pending.result(cast=False)
             except Exception:
                 pass
+            dgs.ops._stream_wait(self._st[w], cur)
         self._exhausted = True
 
     def __del__(self):
@@ -146,3 +161,4 @@ class PrefetchLoader:
             self.close()
         except Exception:
             pass
+

@@ -46,6 +46,8 @@ _SIGS = {
     "dgs_host_register": (c_int, [c_vp, c_i64]),
     "dgs_host_unregister": (c_int, [c_vp]),
     "dgs_index_select": (c_int, [c_vp, c_i64, c_vp, c_int, c_i64, c_vp, c_vp]),
+    "dgs_index_select_device": (c_int, [c_vp, c_i64, c_vp, c_int, c_i64, c_vp, c_vp]),
+    "dgs_stream_wait": (c_int, [c_vp, c_vp]),
     "dgs_sample_neighbors": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp,
                                      p_i64, c_vp]),
     "dgs_relabel": (c_int, [p_vp, p_i64, c_int, p_vp, p_i64, c_int, c_vp, p_i64, p_vp, c_vp]),

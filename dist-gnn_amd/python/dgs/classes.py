@@ -113,8 +113,16 @@ class P2PCacheSampler:
         until result()."""
         if launch_seeds is not None and len(launch_seeds) != len(fan_out):
             raise RuntimeError("launch_seeds needs one seed per hop")
-        s, L, fo, caps, total, buf, ptrs = self._prepare(seeds, fan_out)
-        st = stream_ptr(s.device)
+        prep = self._prepare(seeds, fan_out)
+        return self._begin_prepared(seeds, prep, replace, launch_seeds, host_async,
+                                    stream_ptr(prep[0].device))
+
+    def _begin_prepared(self, seeds, prep, replace, launch_seeds, host_async, stream):
+        """Enqueues a call whose int64 seeds and output buffer _prepare made, on `stream`
+        (a c_void_p or int HIP stream).  PrefetchLoader allocates on the caller's stream and
+        orders the batch stream after those allocations before it launches."""
+        s, L, fo, caps, total, buf, ptrs = prep
+        st = stream if isinstance(stream, c_vp) else c_vp(stream)
         ls = None
         if L and launch_seeds is not None:
             ls = (ctypes.c_uint64 * L)(*[int(x) & 0xFFFFFFFFFFFFFFFF for x in launch_seeds])
@@ -156,7 +164,7 @@ class P2PCacheSampler:
         buf = torch.empty(max(total, 1), dtype=torch.int64, device=s.device)
         return s, L, fo, caps, total, buf, plan_ptrs(buf.data_ptr(), caps)
 
-    def _views(self, seeds, buf, caps, total, sizes, L):
+    def _views(self, seeds, buf, caps, total, sizes, L, cast=True):
         # all views in one split: [U_h, pad, nnz_h, pad, nnz_h, pad] per hop
         lens = []
         for h, (f, e) in enumerate(caps):
@@ -169,7 +177,7 @@ class P2PCacheSampler:
         parts = buf.split(lens)
         out = []
         cur = seeds
-        cast = self._id_dtype != torch.int64
+        cast = cast and self._id_dtype != torch.int64
         for h in range(L):
             fr, r, c = parts[6 * h], parts[6 * h + 2], parts[6 * h + 4]
             if cast:
@@ -254,6 +262,16 @@ class P2PCacheFeatureServer:
                                             c_vp(out.data_ptr()), stream_ptr(n.device)))
         return out
 
+    def _get_feature_alloc(self, nids):
+        """Loader fast path, part 1: the output of _get_feature_into (current stream)."""
+        return torch.empty((nids.numel(), self._stride), dtype=self._dtype, device=nids.device)
+
+    def _get_feature_into(self, nids, out, stream):
+        """Loader fast path, part 2: gather of int64 contiguous device `nids` into `out` on HIP
+        stream `stream` (int)."""
+        check(lib.dgs_feature_server_gather(self._h, c_vp(nids.data_ptr()), nids.numel(),
+                                            c_vp(out.data_ptr()), c_vp(stream)))
+
     def _layout(self):
         """ADDITIVE: -1 = address-table gather, w >= 0 = strided layout over 2^w GPUs."""
         w = ctypes.c_int()
@@ -276,7 +294,9 @@ class _PendingSample:
         self._L, self._caps, self._total, self._buf, self._stream = L, caps, total, buf, stream
         self._out = None
 
-    def result(self):
+    def result(self, cast=True):
+        """cast=False leaves int32-id graphs' blocks as int64 (the caller casts them once its
+        stream is ordered after the call's)."""
         if self._out is None:
             if self._L == 0:
                 self._out = []
@@ -284,6 +304,6 @@ class _PendingSample:
                 sizes = (c_i64 * (3 * self._L))()
                 check(lib.dgs_sampler_sample_end(self._owner._h, self._L, sizes, self._stream))
                 self._out = self._owner._views(self._seeds, self._buf, self._caps, self._total,
-                                               sizes, self._L)
+                                               sizes, self._L, cast)
             self._s64 = self._buf = None
         return self._out

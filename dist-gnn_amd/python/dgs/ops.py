@@ -224,6 +224,22 @@ def _CAPI_cuda_index_select(data, nid):
     return out
 
 
+def _index_select_into(data, nid, out, stream):
+    """Loader fast path: out = data[nid] for contiguous device tensors `data`
+    (int32/int64/float32), int64 `nid` and `out`, on HIP stream `stream` (int)."""
+    rb = data.element_size()
+    for d in data.shape[1:]:
+        rb *= int(d)
+    check(lib.dgs_index_select_device(ctypes.c_void_p(data.data_ptr()), rb,
+                                      ctypes.c_void_p(nid.data_ptr()), 8, nid.numel(),
+                                      ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))
+
+
+def _stream_wait(producer, consumer):
+    """ADDITIVE: HIP stream `consumer` waits for the work enqueued on `producer` so far (ints)."""
+    check(lib.dgs_stream_wait(ctypes.c_void_p(producer), ctypes.c_void_p(consumer)))
+
+
 # ------------------------------------------------------------------ cache helpers
 def _Test_ExtractIndptr(nids, indptr):
     """utils.cu:12-42."""

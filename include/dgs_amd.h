@@ -81,6 +81,14 @@ int dgs_host_unregister(void *ptr);
 int dgs_index_select(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
                      int64_t n, void *out, void *stream);
 
+/* ADDITIVE: dgs_index_select for callers that know data and nid are device memory (no
+ * pointer-attribute queries: the per-batch loader path). */
+int dgs_index_select_device(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
+                            int64_t n, void *out, void *stream);
+/* ADDITIVE: `consumer` waits (on the device) for the work enqueued on `producer` so far -- an
+ * event record + stream wait in one call (DistGNN.dataloading.PrefetchLoader). */
+int dgs_stream_wait(void *producer, void *consumer);
+
 /* replaces sampling::cuda::RowWiseSamplingUniformCUDA (rowwise_sampling.cu:143-189) and,
  * when probs != NULL, RowWiseSamplingBiasCUDA (rowwise_sampling_bias.cu:226-288)
  * (_CAPI_cuda_sample_neighbors / _CAPI_cuda_sample_neighbors_bias).  Draws one launch seed
