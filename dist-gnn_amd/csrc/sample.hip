@@ -566,8 +566,27 @@ struct HalfTopK {
         cas(ck, ci, stride, desc == lower);
       }
     }
-    // top 32 of list + candidates: pairwise best against the reversed candidates (bitonic),
-    // then a descending bitonic merge
+    merge_sorted(ck, ci, k, l);
+  }
+  // Candidates that already form a bitonic sequence over the 32 lanes -- one list sorted
+  // descending (sorted=true: nothing to do), or a descending list in lanes 0-15 followed by an
+  // ascending one in 16-31 (one bitonic merge) -- skip the candidate sort.  Dropping the
+  // entries that do not beat thr keeps either shape.
+  __device__ __forceinline__ void push_bitonic(float key_i, int32_t i, bool valid, int64_t k,
+                                               int l, bool sorted) {
+    const bool cand = valid && ares_better(key_i, i, thr_k, thr_i);
+    if (!half_ballot(cand)) return;
+    float ck = cand ? key_i : -__builtin_inff();
+    int32_t ci = cand ? i : INT32_MAX;
+    if (!sorted) {
+#pragma unroll
+      for (int stride = 16; stride > 0; stride >>= 1) cas(ck, ci, stride, (l & stride) == 0);
+    }
+    merge_sorted(ck, ci, k, l);
+  }
+  // top 32 of the list and 32 candidates sorted descending: pairwise best against the
+  // reversed candidates (a bitonic sequence), then a descending bitonic merge
+  __device__ __forceinline__ void merge_sorted(float ck, int32_t ci, int64_t k, int l) {
     const float rk = __shfl(ck, 31 - l, 32);
     const int32_t ri = __shfl(ci, 31 - l, 32);
     if (ares_better(rk, ri, bk, bi)) {
@@ -930,7 +949,6 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
 __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
   __shared__ float s_key[8][32];
   __shared__ int32_t s_idx[8][32];
-  __shared__ int s_cnt[8];
   const int64_t S = a.Sc.get();
   const uint64_t packed = (uint64_t)*a.hub.count;
   const int64_t H = (int64_t)(packed >> kHubShift);
@@ -945,35 +963,54 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
     const int per = k <= 16 ? 2 : 1;
     const int part = per == 2 ? (l >> 4) : 0;
     const int e = per == 2 ? (l & 15) : l;
+    // a worker's list is sorted (descending); the second list of a pair is read in reverse
+    // so the 32 lanes hold a bitonic sequence
+    const int er = part ? 15 - e : e;
     for (int64_t w0 = wf + (int64_t)per * g; w0 <= wl; w0 += 8 * per) {
       const int64_t w = w0 + part;
       bool have = w <= wl && bias_worker_c0(total, w, nw) != bias_worker_c0(total, w + 1, nw);
       const int64_t slot = w + h;
       const int n = have ? a.ccnt[slot] : 0;
-      const bool valid = e < n;
+      const bool valid = er < n;
       float key_i = -__builtin_inff();
       int32_t i = INT32_MAX;
       if (valid) {
-        key_i = a.ckey[slot * k + e];
-        i = a.cidx[slot * k + e];
+        key_i = a.ckey[slot * k + er];
+        i = a.cidx[slot * k + er];
       }
-      top.push(key_i, i, valid, k, l);
+      top.push_bitonic(key_i, i, valid, k, l, per == 1);
     }
-    s_key[g][l] = top.bk;
-    s_idx[g][l] = top.bi;
-    if (l == 0) s_cnt[g] = top.cnt;
+    // the 8 half-waves' lists (sorted, only the first k count: an entry past its own list's
+    // k-th can not be among the k best of the union) merged pairwise in a tree
+    const bool mine = l < k && top.bi != INT32_MAX;
+    s_key[g][l] = mine ? top.bk : -__builtin_inff();
+    s_idx[g][l] = mine ? top.bi : INT32_MAX;
     __syncthreads();
-    if (g == 0) {
-      HalfTopK fin;
-      for (int gg = 0; gg < 8; ++gg) {
-        const int n = s_cnt[gg];
-        fin.push(s_key[gg][l], s_idx[gg][l], l < n, k, l);
+#pragma unroll
+    for (int step = 1; step < 8; step <<= 1) {
+      if ((g & (2 * step - 1)) == 0) {
+        float mk = s_key[g][l];
+        int32_t mi = s_idx[g][l];
+        const float ok = s_key[g + step][31 - l];
+        const int32_t oi = s_idx[g + step][31 - l];
+        if (ares_better(ok, oi, mk, mi)) {
+          mk = ok;
+          mi = oi;
+        }
+#pragma unroll
+        for (int stride = 16; stride > 0; stride >>= 1)
+          HalfTopK::cas(mk, mi, stride, (l & stride) == 0);
+        s_key[g][l] = mk;
+        s_idx[g][l] = mi;
       }
+      __syncthreads();
+    }
+    if (g == 0) {
       const int64_t r = a.hub.row[h];
       const RowInfo ri = a.rowinfo[r];
       const int64_t out = a.boff[r / kTileRows] + a.tpre[r];
       if (l < k) {
-        const int64_t v = ri.ptr[fin.bi];
+        const int64_t v = ri.ptr[s_idx[0][l]];
         a.rowpos[out + l] = r;
         a.col[out + l] = v;
         table_record(a.table, v, S + out + l);
