@@ -527,6 +527,10 @@ __device__ __forceinline__ T float_max(T a, T b) {
 }
 
 constexpr int kBiasRowsPerBlock = kTileRows / 32;  // one 32-lane half-wave per row
+#ifndef DGS_SPARSE_PUSH
+#define DGS_SPARSE_PUSH 10
+#endif
+constexpr int kSparsePush = DGS_SPARSE_PUSH;  // candidate batches up to this size are inserted one by one
 
 // Half-wave top-k under the total order (key desc, edge index asc): lane q holds the q-th best
 // (key, idx) so far (a sorted list of 32; the first k count), thr = the k-th best.  A step's
@@ -551,9 +555,35 @@ struct HalfTopK {
       i = pi;
     }
   }
+  // One candidate (ck, ci), the same on every lane, into the sorted list: the entries that
+  // beat it are a prefix of length pos; the rest move down a lane (the 32nd drops out).
+  __device__ __forceinline__ void insert_one(float ck, int32_t ci, int l) {
+    const int pos = __builtin_popcount(half_ballot(ares_better(bk, bi, ck, ci)));
+    const float uk = __shfl_up(bk, 1, 32);
+    const int32_t ui = __shfl_up(bi, 1, 32);
+    if (l > pos) {
+      bk = uk;
+      bi = ui;
+    } else if (l == pos) {
+      bk = ck;
+      bi = ci;
+    }
+  }
   __device__ __forceinline__ void push(float key_i, int32_t i, bool valid, int64_t k, int l) {
     const bool cand = valid && ares_better(key_i, i, thr_k, thr_i);
-    if (!half_ballot(cand)) return;
+    uint32_t m = half_ballot(cand);
+    if (!m) return;
+    if (__builtin_popcount(m) <= kSparsePush) {
+      // few candidates: insert them one by one (a broadcast, a ballot and a lane shift each)
+      // instead of sorting 32 lanes -- the same top-32 list either way
+      do {
+        const int src = __builtin_ctz(m);
+        m &= m - 1;
+        insert_one(__shfl(key_i, src, 32), __shfl(i, src, 32), l);
+      } while (m);
+      update_thr(k, l);
+      return;
+    }
     float ck = cand ? key_i : -__builtin_inff();
     int32_t ci = cand ? i : INT32_MAX;
     // bitonic sort of the candidates, descending
@@ -595,6 +625,9 @@ struct HalfTopK {
     }
 #pragma unroll
     for (int stride = 16; stride > 0; stride >>= 1) cas(bk, bi, stride, (l & stride) == 0);
+    update_thr(k, l);
+  }
+  __device__ __forceinline__ void update_thr(int64_t k, int l) {
     cnt = __builtin_popcount(half_ballot(l < k && bi != INT32_MAX));
     thr_k = __shfl(bk, (int)(k - 1), 32);
     thr_i = __shfl(bi, (int)(k - 1), 32);
