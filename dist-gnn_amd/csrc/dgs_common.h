@@ -150,6 +150,18 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
   return c;
 }
 
+// Issue priority of the latency-bound per-hop kernels (prep, row sampling, compaction,
+// relabel) over co-resident waves of the throughput-bound hub kernels of other batches in
+// flight (s_setprio; 0 = the hardware default).
+#ifndef DGS_LAT_PRIO
+#define DGS_LAT_PRIO 1
+#endif
+__device__ __forceinline__ void latency_prio() {
+#if DGS_LAT_PRIO
+  __builtin_amdgcn_s_setprio(DGS_LAT_PRIO);
+#endif
+}
+
 // Wave-uniform 64-bit value -> scalar registers.
 __device__ __forceinline__ uint64_t wave_uniform(uint64_t v) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);

@@ -132,6 +132,9 @@ struct StridedSrc {
   }
 };
 
+#ifndef DGS_GATHER_PRIO
+#define DGS_GATHER_PRIO 1
+#endif
 #ifndef DGS_GATHER_UNROLL
 #define DGS_GATHER_UNROLL 4
 #endif
@@ -147,6 +150,11 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nch
                                                            char *__restrict__ out,
                                                            uint64_t *stamp) {
   using T = typename VecT<V>::T;
+#if DGS_GATHER_PRIO
+  // issue priority over co-resident waves of other kernels (the sampler's VALU-bound waves
+  // share the SIMDs in the pipeline): this wave's loads and stores go out first
+  __builtin_amdgcn_s_setprio(DGS_GATHER_PRIO);
+#endif
   // profiling only (stamp != nullptr, a kernel argument: uniform branch)
   if (stamp && threadIdx.x == 0) stamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   const uint32_t base = blockIdx.x * (uint32_t)(kGatherThreads * kGatherUnroll) + threadIdx.x;

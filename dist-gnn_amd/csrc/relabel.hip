@@ -154,6 +154,7 @@ __device__ __forceinline__ int64_t first_flags(const int64_t *a, int64_t na, con
 __global__ __launch_bounds__(kThreads) void k_dcount(const int64_t *a, Count nac,
                                                      const int64_t *b, const int64_t *d_nb,
                                                      Table t, int64_t *tcnt) {
+  latency_prio();
   __shared__ int64_t lds[kThreads / 64];
   const int64_t na = nac.get();
   const int64_t n = na + *d_nb;
@@ -171,6 +172,7 @@ __global__ __launch_bounds__(kThreads) void k_dscatter(const int64_t *a, Count n
                                                        Table t, const int64_t *tcnt,
                                                        int64_t *unique, int64_t *d_nunique,
                                                        HostSizes pub) {
+  latency_prio();
   __shared__ int64_t lds[kThreads / 64];
   const int64_t na = nac.get();
   const int64_t n = na + *d_nb;
@@ -202,6 +204,7 @@ __global__ __launch_bounds__(kThreads) void k_dscatter(const int64_t *a, Count n
 }
 
 __global__ __launch_bounds__(kThreads) void k_drelabel_hop(RelabelTail r) {
+  latency_prio();
   relabel_tail_block(r, blockIdx.x);
 }
 

@@ -214,11 +214,15 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
 
 // Prep: per-row lookup (one 16-byte node-table load), in-tile output prefix, tile sums, hub
 // registration, relabel insert of the seeds.
-__global__ __launch_bounds__(kTileRows) void k_prep(PrepArgs a) { prep_block(a, blockIdx.x); }
+__global__ __launch_bounds__(kTileRows) void k_prep(PrepArgs a) {
+  latency_prio();
+  prep_block(a, blockIdx.x);
+}
 
 // The previous hop's relabel pass (blocks [0, tail.nblk), on the other relabel table) and this
 // hop's prep in one launch: both only need the previous hop's unique frontier.
 __global__ __launch_bounds__(kTileRows) void k_prep_tail(PrepArgs a, RelabelTail tail) {
+  latency_prio();
   if ((int64_t)blockIdx.x < tail.nblk)
     relabel_tail_block(tail, blockIdx.x);
   else
@@ -460,6 +464,7 @@ __global__ __launch_bounds__(256) void k_hub_reservoir(UniformArgs a, const int6
 
 template <bool kReplace>
 __global__ __launch_bounds__(kTileRows) void k_sample_uniform(UniformArgs a, int use_hubs) {
+  latency_prio();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   sample_rows<kReplace>(a, blockIdx.x, reinterpret_cast<int32_t *>(smem), use_hubs != 0);
 }
