@@ -235,6 +235,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_hop(const int64_t *bsum,
                                                           const int64_t *tsum, Count Sc,
                                                           int64_t *boff, int64_t *tboff,
                                                           int64_t *d_nnz, int64_t *d_cdf_total) {
+  latency_prio();
   __shared__ int64_t lds[kScanThreads / 64];
   const int64_t nb = (Sc.get() + kTileRows - 1) / kTileRows;
   for (int pass = 0; pass < 2; ++pass) {
@@ -685,6 +686,7 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
     const int32_t *__restrict__ tpre2, const int64_t *__restrict__ tboff, float *cdf,
     int64_t *__restrict__ rowpos, int64_t *__restrict__ col, Table table,
     const int64_t *__restrict__ hubid) {
+  latency_prio();
   const int64_t S = Sc.get();
   const int64_t G = (S + 15) / 16;  // reference grid: ceil(S / TILE_SIZE=16)
   const int hw = threadIdx.x >> 5, l = threadIdx.x & 31;
@@ -985,6 +987,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
 // One workgroup per hub row: its 8 half-waves reduce interleaved subsets of the row's worker
 // slots, then half-wave 0 merges the 8 partial lists and emits the picks.
 __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
+  latency_prio();
   __shared__ float s_key[8][32];
   __shared__ int32_t s_idx[8][32];
   const int64_t S = a.Sc.get();
