@@ -159,13 +159,14 @@ int dgs_index_select_device(const void *data, int64_t row_bytes, const void *nid
 
 int dgs_stream_wait(void *producer, void *consumer) {
   return guard([&] {
-    // one event per calling thread: a wait already enqueued keeps the record it saw, so the
-    // event can be recorded again at once
-    thread_local hipEvent_t ev = [] {
-      hipEvent_t e;
-      DGS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      return e;
-    }();
+    // one event per calling thread and device: a wait already enqueued keeps the record it
+    // saw, so the event can be recorded again at once
+    thread_local std::vector<hipEvent_t> evs;
+    int dev = 0;
+    DGS_HIP(hipGetDevice(&dev));
+    if ((int)evs.size() <= dev) evs.resize((size_t)dev + 1, nullptr);
+    if (!evs[dev]) DGS_HIP(hipEventCreateWithFlags(&evs[dev], hipEventDisableTiming));
+    hipEvent_t ev = evs[dev];
     DGS_HIP(hipEventRecord(ev, S(producer)));
     DGS_HIP(hipStreamWaitEvent(S(consumer), ev, 0));
   });
