@@ -319,20 +319,27 @@ __device__ __forceinline__ void hub_reservoir(const UniformArgs &a, int64_t gw, 
   if (c0 >= c1) return;
   int64_t h = group_search<64>(hub.cptr, H, c0);  // largest h with cptr[h] <= c0
   int64_t hstart = hub.cptr[h], hnext = h + 1 < H ? hub.cptr[h + 1] : total;
-  int64_t r = hub.row[h];
-  int64_t deg = ri_deg(a.rowinfo[r]);
+  // per-row values, made wave-uniform once per row (scalar key and slot address: nothing of
+  // the row is recomputed per chunk)
+  int64_t r = 0, deg = 0;
+  uint2 kk;
+  int32_t *sl = nullptr;
+  auto load_row = [&]() {
+    r = (int64_t)wave_uniform((uint64_t)hub.row[h]);
+    deg = (int64_t)wave_uniform((uint64_t)ri_deg(a.rowinfo[r]));
+    const uint64_t key = a.seed * (uint64_t)S + (uint64_t)r;
+    kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
+    sl = a.hubslot + r * k;
+  };
+  load_row();
   for (int64_t c = c0; c < c1; ++c) {
     while (c >= hnext) {
       ++h;
       hstart = hnext;
       hnext = h + 1 < H ? hub.cptr[h + 1] : total;
-      r = hub.row[h];
-      deg = ri_deg(a.rowinfo[r]);
+      load_row();
     }
     const int64_t q = c - hstart;
-    const uint64_t key = wave_uniform(a.seed * (uint64_t)S + (uint64_t)r);
-    const uint2 kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
-    int32_t *sl = a.hubslot + r * k;
     const uint4 o4a = philox4x32_10(
         make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), (uint32_t)lane, 0u), kk);
     const uint4 o4b = philox4x32_10(
