@@ -200,3 +200,36 @@ def test_begin_end_protocol(dgs, host_async):
                                       dgs._lib.stream_ptr(torch.device("cuda", 0))) != 0
     again = sampler._CAPI_sample_node_classifiction(s, [10, 5], False)
     assert again[0][1].numel() > 0
+
+
+def test_prefetch_outputs_survive_caller_memory_reuse(dgs):
+    """Outputs are allocated on the caller's stream and written on batch streams ordered after
+    it: a caller that drops each batch at once and fills freshly allocated memory on its stream
+    (a training step recycling the blocks) must not corrupt the batches still in flight, and a
+    loader closed mid-way leaves the memory it dropped safe to reuse."""
+    from DistGNN.dataloading import PrefetchLoader
+    _, sampler, server, labels, _ = _services(dgs, False)
+    fan_out = [15, 10, 5]
+    batches = _batches(labels.numel(), nb=12)
+    dgs.ops._CAPI_set_random_seed(5)
+    exp = _sequential(dgs, sampler, server, labels, batches, fan_out)
+    dgs.ops._CAPI_set_random_seed(5)
+    kept = []
+    for blocks, x, y in PrefetchLoader(sampler, batches, fan_out, server=server, labels=labels,
+                                       depth=3):
+        kept.append(([tuple(t.clone() for t in b) for b in blocks], x.clone(), y.clone()))
+        del blocks, x, y
+        junk = torch.full((1 << 22,), -7, dtype=torch.int64, device="cuda")  # reuses freed blocks
+        junk.add_(1)
+        del junk
+    torch.cuda.synchronize()
+    for a, b in zip(kept, exp):
+        _same(a, b)
+    # closed after two of twelve batches: the in-flight calls end, their memory is recycled
+    loader = iter(PrefetchLoader(sampler, batches, fan_out, server=server, labels=labels, depth=3))
+    next(loader)
+    next(loader)
+    loader.close()
+    junk = torch.full((1 << 22,), 3, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    assert int(junk.min()) == 3 and int(junk.max()) == 3
