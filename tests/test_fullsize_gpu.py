@@ -5,6 +5,7 @@ of 1024 seeds with fan-out [15, 10, 5] run through PrefetchLoader with 3 batches
 
 - bit-exact against the oracle (oracle/dgs_oracle.c via oracle.py) for a few batches, uniform
   and degree-weighted biased: frontiers, relabelled COO, gathered features and labels;
+- with replacement (uniform and biased), two batches each, bit-exact;
 - configs[4]'s RMAT-1B shape (scale 26, edge factor 16: 67 M nodes, 1.07 B edges, d = 256): two
   pipelined batches bit-exact, uniform and biased, features included;
 - size-independent properties over many batches: every frontier starts with its seeds and has
@@ -65,11 +66,11 @@ def _services(dgs, P, bias):
     return sampler, server
 
 
-def _pipelined(dgs, sampler, server, labels, batches):
+def _pipelined(dgs, sampler, server, labels, batches, replace=False):
     from DistGNN.dataloading import PrefetchLoader
     out = []
-    for blocks, x, y in PrefetchLoader(sampler, batches, FAN_OUT, server=server, labels=labels,
-                                       depth=3):
+    for blocks, x, y in PrefetchLoader(sampler, batches, FAN_OUT, replace=replace, server=server,
+                                       labels=labels, depth=3):
         out.append((blocks, x, y))
     torch.cuda.synchronize()
     return out
@@ -99,6 +100,26 @@ def test_products_pipeline_bit_exact(dgs, products, bias):
         front = exp[-1][1]
         assert np.array_equal(x.cpu().numpy().view(np.uint32), feats[front].view(np.uint32))
         assert np.array_equal(y.cpu().numpy(), labels[seeds])
+
+
+@pytest.mark.parametrize("bias", [False, True])
+def test_products_with_replacement_bit_exact(dgs, products, bias):
+    """K3 (uniform) and K6 (biased CDF + upper_bound) with replacement at full size."""
+    P = products
+    sampler, server = _services(dgs, P, bias)
+    batches = _batches(P["train"], 2, seed=9)
+    dgs.ops._CAPI_set_random_seed(404)
+    got = _pipelined(dgs, sampler, server, P["labels"], batches, replace=True)
+    ls = O.launch_seeds(404, len(FAN_OUT) * 2)
+    ip, ix = P["indptr"].numpy(), P["indices"].numpy()
+    pr = P["probs"].numpy() if bias else None
+    for b, (blocks, x, y) in enumerate(got):
+        exp = O.node_classification_sample(batches[b].cpu().numpy(), ip, ix, FAN_OUT, True,
+                                           ls[3 * b:3 * b + 3], probs=pr)
+        for (gs, gf, gr, gc), (es, ef, er, ec) in zip(blocks, exp):
+            assert np.array_equal(gf.cpu().numpy(), ef)
+            assert np.array_equal(gr.cpu().numpy(), er)
+            assert np.array_equal(gc.cpu().numpy(), ec)
 
 
 def test_products_pipeline_properties(dgs, products):
