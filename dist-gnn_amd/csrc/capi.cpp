@@ -3,6 +3,9 @@
 #include "../../include/dgs_amd.h"
 
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -48,9 +51,28 @@ T *dev_ptr(T *p, const char *what) {
   return p;
 }
 
-HopScratch &op_scratch() {
-  static HopScratch ws;
-  return ws;
+// Scratch of the standalone ops (dgs_sample_neighbors, dgs_relabel), one per (device, stream):
+// calls on different streams or threads never share buffers, calls on one stream are ordered
+// by the stream, and the returned lock serialises the host side of calls on one stream.  (The
+// reference allocates per call through the caching allocator.)
+struct OpScratch {
+  std::mutex mu;
+  HopScratch ws;
+};
+std::unique_lock<std::mutex> op_scratch(hipStream_t st, HopScratch **ws) {
+  static std::mutex m;
+  static std::map<std::pair<int, hipStream_t>, std::unique_ptr<OpScratch>> all;
+  int dev = 0;
+  DGS_HIP(hipGetDevice(&dev));
+  OpScratch *o;
+  {
+    std::lock_guard<std::mutex> g(m);
+    std::unique_ptr<OpScratch> &p = all[{dev, st}];
+    if (!p) p.reset(new OpScratch);
+    o = p.get();
+  }
+  *ws = &o->ws;
+  return std::unique_lock<std::mutex>(o->mu);
 }
 }  // namespace
 
@@ -186,7 +208,9 @@ int dgs_sample_neighbors(const int64_t *seeds, int64_t Sn, const int64_t *indptr
     src.probs.p[0] = dev_ptr(probs, "probs");
     src.num_nodes = INT64_MAX;  // no node count at this boundary (reference: unchecked)
     seeds = dev_ptr(seeds, "seeds");
-    HopScratch &ws = op_scratch();
+    HopScratch *wsp = nullptr;
+    const std::unique_lock<std::mutex> lk = op_scratch(st, &wsp);
+    HopScratch &ws = *wsp;
     int64_t *tmp = nullptr;  // [0] = nnz, then rowpos[S*k]
     const int64_t cap = Sn * num_picks;
     DGS_HIP(hipMallocAsync((void **)&tmp, sizeof(int64_t) * (size_t)(cap + 1), st));
@@ -226,7 +250,9 @@ int dgs_relabel(const int64_t *const *maps, const int64_t *map_sizes, int n_maps
       off += req_sizes[i];
     }
     int64_t *d_cnt = buf + nm + 2 * nr;
-    relabel_generic(buf, nm, buf + nm, nr, unique_out, buf + nm + nr, d_cnt, op_scratch(), st);
+    HopScratch *ws = nullptr;
+    const std::unique_lock<std::mutex> lk = op_scratch(st, &ws);
+    relabel_generic(buf, nm, buf + nm, nr, unique_out, buf + nm + nr, d_cnt, *ws, st);
     off = nm + nr;
     for (int i = 0; i < n_reqs; ++i) {
       if (req_sizes[i] > 0)
@@ -279,12 +305,21 @@ int dgs_compute_frontier_heat_fixed(const int64_t *seeds, int64_t n_seeds,
                                     float *frontier_heat, void *stream) {
   return guard([&] {
     hipStream_t st = S(stream);
-    HopScratch &ws = op_scratch();
-    ws.misc.ensure(sizeof(uint64_t) * (size_t)(num_nodes > 0 ? num_nodes : 1));
-    heat(dev_ptr(seeds, "seeds"), n_seeds, dev_ptr(indptr, "indptr"),
-         dev_ptr(indices, "indices"), dev_ptr(probs, "probs"), dev_ptr(seeds_heat, "seeds_heat"),
-         num_picks, indptr_diff, frontier_heat, num_nodes, ws.misc.as<unsigned long long>(),
-         st);
+    // the int64 accumulator is this call's own (stream-ordered allocation, freed behind the
+    // kernels that use it): nothing another op or stream runs can overwrite it
+    unsigned long long *acc = nullptr;
+    DGS_HIP(hipMallocAsync((void **)&acc,
+                           sizeof(uint64_t) * (size_t)(num_nodes > 0 ? num_nodes : 1), st));
+    try {
+      heat(dev_ptr(seeds, "seeds"), n_seeds, dev_ptr(indptr, "indptr"),
+           dev_ptr(indices, "indices"), dev_ptr(probs, "probs"),
+           dev_ptr(seeds_heat, "seeds_heat"), num_picks, indptr_diff, frontier_heat, num_nodes,
+           acc, st);
+    } catch (...) {
+      (void)hipFreeAsync(acc, st);
+      throw;
+    }
+    DGS_HIP(hipFreeAsync(acc, st));
   });
 }
 

@@ -2,6 +2,8 @@
 #include "context.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "dgs_ops.h"
@@ -307,17 +309,40 @@ void profile_collect() {
     DGS_HIP(hipGetDevice(&dev));
     DGS_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
     std::vector<uint64_t> h;
+    // DGS_PROF_DETAIL=1: per measurement, how a launch's span splits into the dispatch spread
+    // (first to last workgroup start) and the workgroups' own durations (stderr, diagnostics)
+    static const bool detail = getenv("DGS_PROF_DETAIL") != nullptr;
+    double d_span[3] = {0, 0, 0}, d_spread[3] = {0, 0, 0}, d_wg[3] = {0, 0, 0};
+    int64_t d_n[3] = {0, 0, 0};
     for (auto &r : sr) {
       h.resize((size_t)(2 * r.nblocks));
       DGS_HIP(hipMemcpy(h.data(), r.buf, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost));
-      uint64_t t0 = ~0ull, t1 = 0;
+      uint64_t t0 = ~0ull, t1 = 0, s1 = 0;
+      double wg = 0;
       for (int64_t b = 0; b < r.nblocks; ++b) {
         t0 = h[2 * b] < t0 ? h[2 * b] : t0;
         t1 = h[2 * b + 1] > t1 ? h[2 * b + 1] : t1;
+        s1 = h[2 * b] > s1 ? h[2 * b] : s1;
+        wg += (double)(h[2 * b + 1] - h[2 * b]);
       }
-      if (t1 > t0 && khz > 0) add_measure(r.which, (double)(t1 - t0) / (double)khz);
+      if (t1 > t0 && khz > 0) {
+        add_measure(r.which, (double)(t1 - t0) / (double)khz);
+        if (detail && r.which >= 0 && r.which < 3) {
+          d_span[r.which] += (double)(t1 - t0) / khz;
+          d_spread[r.which] += (double)(s1 - t0) / khz;
+          d_wg[r.which] += wg / (double)r.nblocks / khz;
+          d_n[r.which] += 1;
+        }
+      }
       if (r.own) stamp_pool().push_back({r.nblocks, r.buf});
     }
+    for (int w = 0; detail && w < 3; ++w)
+      if (d_n[w])
+        fprintf(stderr,
+                "[dgs prof] which=%d launches=%lld avg span %.2f us, dispatch spread %.2f us, "
+                "workgroup duration %.2f us\n",
+                w, (long long)d_n[w], 1e3 * d_span[w] / d_n[w], 1e3 * d_spread[w] / d_n[w],
+                1e3 * d_wg[w] / d_n[w]);
     sr.clear();
     stamp_slab().used = 0;
   }

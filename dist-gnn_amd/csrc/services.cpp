@@ -190,6 +190,12 @@ void Sampler::bounds(int64_t n_seeds, const int64_t *fan_out, int L, int64_t *fc
   int64_t s = n_seeds;
   for (int h = 0; h < L; ++h) {
     const int64_t k = fan_out[L - 1 - h];
+    DGS_CHECK(k >= 0, "fan_out entries must be non-negative");
+    // The relabel tables record positions in cat(seeds, col) as int32 (kTableNoPos = INT32_MAX
+    // is the empty mark): every position of the hop must stay below it.
+    DGS_CHECK(k == 0 || s <= (int64_t)(INT32_MAX - 1 - s) / k,
+              "one hop of this call could hold 2^31 - 1 or more seeds + sampled edges "
+              "(relabel positions are 32-bit): split the seed batch");
     const int64_t e = s * k;
     ecap[h] = e;
     s = s + e;

@@ -19,22 +19,29 @@ from dgs._lib import _raw_stream
 
 __all__ = ["PrefetchLoader"]
 
-# Streams are reused by every loader on a device: the sampler keeps one sampling context
-# (scratch, relabel tables: 16 B per node) per stream for its lifetime, and a context's first
-# use allocates it.
-_STREAMS = {}
+# Batch streams are pooled per device and checked out by one loader at a time: the sampler
+# keeps one sampling context (scratch, relabel tables: 16 B per node) per stream for its
+# lifetime and allows one outstanding call per stream, so two live loaders over one sampler
+# (zipped, nested, or one left open) must not share a stream.  A loader returns its streams in
+# close(); a stream's first use by the sampler allocates its context.
+_FREE_STREAMS = {}
 # DGS_PREFETCH_SYNC=1: issue each batch's launches on the caller's thread (experiments)
 _HOST_ASYNC = os.environ.get("DGS_PREFETCH_SYNC", "0") != "1"
 _STREAMS_LOCK = threading.Lock()
 
 
-def _worker_streams(device, n):
+def _checkout_streams(device, n):
     with _STREAMS_LOCK:
-        pool = _STREAMS.setdefault(device, [])
-        while len(pool) < n:
-            pool.append(torch.cuda.Stream(device=device))
-        return pool[:n]
+        free = _FREE_STREAMS.setdefault(device, [])
+        out = [free.pop() for _ in range(min(n, len(free)))]
+    while len(out) < n:
+        out.append(torch.cuda.Stream(device=device))
+    return out
 
+
+def _return_streams(device, streams):
+    with _STREAMS_LOCK:
+        _FREE_STREAMS.setdefault(device, []).extend(streams)
 
 
 class PrefetchLoader:
@@ -44,11 +51,14 @@ class PrefetchLoader:
     - x = server._CAPI_get_feature(blocks[-1][1]), or None without a server,
     - y = dgs.ops._CAPI_cuda_index_select(labels, seeds), or None without labels.
 
-    Up to `depth` batches are in flight, batch i on stream i mod depth.  Every tensor handed out
-    is ready on the caller's current stream when __next__ returns (that stream waits for the
-    batch's stream; the host does not block on it).  Each batch's per-hop launch seeds are
-    drawn from the global engine in batch order, so the output is exactly that of the
-    sequential loop after the same dgs.ops._CAPI_set_random_seed.
+    Up to `depth` batches are in flight, batch i on the loader's stream i mod depth (streams
+    are the loader's own until close()).  Every tensor handed out is ready on the caller's
+    current stream when __next__ returns (that stream waits for the batch's stream; the host
+    does not block on it); the feature gather itself runs on the caller's stream.  Each
+    batch's per-hop launch seeds are drawn from the global engine by the sampler when it
+    accepts the call, in batch order, so the output is exactly that of the sequential loop
+    after the same dgs.ops._CAPI_set_random_seed (several live loaders draw in the order
+    their batches are submitted).
     """
 
     def __init__(self, sampler, seeds_iter, fan_out, replace=False, server=None, labels=None,
@@ -66,7 +76,7 @@ class PrefetchLoader:
         self.fan_out, self.replace = list(fan_out), bool(replace)
         self._seeds = iter(seeds_iter)
         self._exhausted = False
-        self._streams = _worker_streams(self.device, depth)
+        self._streams = _checkout_streams(self.device, depth)
         self._st = [s.cuda_stream for s in self._streams]
         self._dev = self.device.index
         self._inflight = collections.deque()
@@ -93,7 +103,6 @@ class PrefetchLoader:
         cur = self._caller_stream()
         # the caller may drop its seeds at once: their memory must outlive B's reads
         seeds.record_stream(self._streams[w])
-        launch_seeds = dgs.ops.draw_launch_seeds(len(self.fan_out))
         prep = self.sampler._prepare(seeds, self.fan_out)  # int64 seeds + outputs, on C
         s64 = prep[0]
         y = None
@@ -104,9 +113,9 @@ class PrefetchLoader:
         if y is not None:  # depends on the seeds only: issued first
             dgs.ops._index_select_into(self.labels, s64, y, st)
         # B is not touched again before result(): the sampler's launcher thread may issue
-        # the launches
-        pending = self.sampler._begin_prepared(seeds, prep, self.replace, launch_seeds,
-                                               _HOST_ASYNC, st)
+        # the launches.  The sampler draws the launch seeds once it has accepted the call.
+        pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, _HOST_ASYNC,
+                                               st)
         self._inflight.append((pending, y, w))
 
     def __iter__(self):
@@ -116,6 +125,7 @@ class PrefetchLoader:
         while not self._exhausted and len(self._inflight) < len(self._st):
             self._submit()
         if not self._inflight:
+            self.close()  # returns the streams
             raise StopIteration
         pending, y, w = self._inflight.popleft()
         st = self._st[w]
@@ -126,13 +136,14 @@ class PrefetchLoader:
             dgs.ops._stream_wait(st, cur)
             self.close()
             raise
+        # C after B (the sample call, the label gather); the feature gather then runs on C,
+        # whose hardware queue the batch streams do not use
+        dgs.ops._stream_wait(st, cur)
         x = None
         if self.server is not None:
             front = blocks[-1][1]
             x = self.server._get_feature_alloc(front)
-            dgs.ops._stream_wait(cur, st)
-            self.server._get_feature_into(front, x, st)
-        dgs.ops._stream_wait(st, cur)
+            self.server._get_feature_into(front, x, cur)
         dt = self.sampler._id_dtype
         if dt != torch.int64:  # int32 graphs: cast on the caller's stream, now ordered after B
             cast, cur_seeds = [], blocks[0][0]
@@ -155,6 +166,9 @@ class PrefetchLoader:
                 pass
             dgs.ops._stream_wait(self._st[w], cur)
         self._exhausted = True
+        if self._streams:
+            _return_streams(self.device, self._streams)
+            self._streams, self._st = [], []
 
     def __del__(self):
         try:

@@ -299,6 +299,30 @@ def test_tensor_p2p_server_local(dgs):
     assert torch.equal(srv._CAPI_get_device_tensor(0), t.flatten())
 
 
+@pytest.mark.parametrize("n_seeds,fan_out,replace", [(1 << 20, [2048], True),
+                                                      (1 << 22, [512], False),
+                                                      (1 << 23, [300], True)])
+def test_sampler_rejects_int32_position_overflow(dgs, n_seeds, fan_out, replace):
+    """Relabel positions are 32-bit: a call whose hop could hold 2^31 - 1 or more seeds +
+    sampled edges (host-side bounds) raises before anything is allocated or launched, and the
+    sampler stays usable."""
+    indptr, indices, _ = _hub_graph(11)
+    n = indptr.size - 1
+    sampler = dgs.classes.P2PCacheSampler(torch.from_numpy(indptr), torch.from_numpy(indices),
+                                          torch.Tensor(), torch.arange(n), 0)
+    seeds = torch.zeros(n_seeds, dtype=torch.int64, device="cuda")
+    with pytest.raises(RuntimeError, match="32-bit"):
+        sampler._CAPI_sample_node_classifiction(seeds, fan_out, replace)
+    small = _cuda(np.random.default_rng(5).permutation(n)[:64])
+    dgs.ops._CAPI_set_random_seed(99)
+    got = sampler._CAPI_sample_node_classifiction(small, [15, 10, 5], False)
+    exp = O.node_classification_sample(small.cpu().numpy(), indptr, indices, [15, 10, 5], False,
+                                       O.launch_seeds(99, 3))
+    for g, e in zip(got, exp):
+        for a, b in zip(g, e):
+            assert np.array_equal(a.cpu().numpy(), b)
+
+
 # ------------------------------------------------------------------ heat
 @pytest.mark.parametrize("bias", [False, True])
 def test_heat_matches_oracle(dgs, bias):
@@ -388,3 +412,55 @@ def test_pinned_tensor_outlives_caller_reference(dgs):
     assert kept.data_ptr() == p and int(kept[-1]) == (1 << 16) - 1
     dgs.ops._CAPI_tensor_unpin_memory(kept)
     assert p not in dgs.ops._registered
+
+
+def test_standalone_ops_on_two_streams(dgs):
+    """The standalone ops keep their scratch per stream and the deterministic heat op its
+    accumulator per call: heat on one stream interleaved with relabel + neighbour sampling on
+    another (two threads) gives exactly what each gives alone."""
+    import threading
+    indptr, indices, probs = _hub_graph(2, giant=False)
+    n = indptr.size - 1
+    ip, ix = _cuda(indptr), _cuda(indices)
+    heat = _cuda(np.random.default_rng(1).random(n).astype(np.float32))
+    hseeds = _cuda(np.random.default_rng(2).permutation(n)[:300])
+    rng = np.random.default_rng(4)
+    maps = [_cuda(rng.integers(0, 300, 4000)), _cuda(rng.integers(0, 600, 9000))]
+    sseeds = _cuda(rng.integers(0, n, 200))
+    reps = 6
+
+    def heat_op():
+        return dgs.ops._CAPI_compute_frontier_heat(hseeds, ip, ix, heat, 5, 0,
+                                                   deterministic=True)
+
+    def other_ops():
+        u, rel = dgs.ops._CAPI_cuda_sampled_tensor_relabel(maps, maps)
+        r, c = dgs.ops._CAPI_cuda_sample_neighbors(sseeds, ip, ix, 10, False)
+        return [u] + list(rel) + [r, c]
+
+    exp_h = heat_op()
+    dgs.ops._CAPI_set_random_seed(8)
+    exp_o = [other_ops() for _ in range(reps)]
+    torch.cuda.synchronize()
+    got_h, got_o = [None] * reps, [None] * reps
+
+    def run(fn, out, seed):
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            if seed is not None:
+                dgs.ops._CAPI_set_random_seed(seed)
+            for i in range(reps):
+                out[i] = fn()
+            st.synchronize()
+
+    ths = [threading.Thread(target=run, args=(heat_op, got_h, None)),
+           threading.Thread(target=run, args=(other_ops, got_o, 8))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for h in got_h:
+        assert torch.equal(h, exp_h)
+    for g, e in zip(got_o, exp_o):
+        for a, b in zip(g, e):
+            assert torch.equal(a, b)

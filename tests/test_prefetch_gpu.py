@@ -233,3 +233,49 @@ def test_prefetch_outputs_survive_caller_memory_reuse(dgs):
     junk = torch.full((1 << 22,), 3, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
     assert int(junk.min()) == 3 and int(junk.max()) == 3
+
+
+def test_two_live_loaders_on_one_sampler(dgs):
+    """Two loaders over one sampler consumed in lock step (zip): each has its own streams, so
+    neither hits the other's outstanding call, and each batch equals the seeded sequential call
+    with the launch seeds of its submission slot (loader A fills its `depth` slots, then B, then
+    they alternate one batch each)."""
+    from DistGNN.dataloading import PrefetchLoader
+    _, sampler, server, labels, _ = _services(dgs, False)
+    fan_out = [15, 10, 5]
+    a_b, b_b = _batches(labels.numel(), nb=6), _batches(labels.numel(), nb=12)[6:]
+    depth = 3
+    dgs.ops._CAPI_set_random_seed(41)
+    got = list(zip(PrefetchLoader(sampler, a_b, fan_out, server=server, labels=labels,
+                                  depth=depth),
+                   PrefetchLoader(sampler, b_b, fan_out, server=server, labels=labels,
+                                  depth=depth)))
+    torch.cuda.synchronize()
+    order = [("a", i) for i in range(depth)] + [("b", i) for i in range(depth)]
+    for i in range(depth, len(a_b)):
+        order += [("a", i), ("b", i)]
+    dgs.ops._CAPI_set_random_seed(41)
+    seeds = {slot: dgs.ops.draw_launch_seeds(len(fan_out)) for slot in order}
+    for i, (ga, gb) in enumerate(got):
+        for which, batches, g in (("a", a_b, ga), ("b", b_b, gb)):
+            s = batches[i]
+            blocks = sampler._sample_seeded(s, fan_out, False, seeds[(which, i)])
+            exp = (blocks, server._CAPI_get_feature(blocks[-1][1]),
+                   dgs.ops._CAPI_cuda_index_select(labels, s))
+            _same(g, exp)
+
+
+def test_loader_streams_are_returned(dgs):
+    """A finished or closed loader gives its streams back; a live one keeps them."""
+    from DistGNN.dataloading import PrefetchLoader
+    from DistGNN.dataloading import prefetch as P
+    _, sampler, server, labels, _ = _services(dgs, False)
+    batches = _batches(labels.numel(), nb=4)
+    first = PrefetchLoader(sampler, batches, [5, 5], server=server, depth=2)
+    second = PrefetchLoader(sampler, batches, [5, 5], server=server, depth=2)
+    assert not {s.cuda_stream for s in first._streams} & {s.cuda_stream for s in second._streams}
+    list(first)
+    assert not first._streams
+    second.close()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    assert len(P._FREE_STREAMS[dev]) >= 4

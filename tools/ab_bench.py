@@ -1,8 +1,11 @@
-"""Same-box A/B of library builds: alternates `bench.py` runs over the given libdgs_amd.so
-files (DGS_AMD_LIB) and prints the median ms/step and sample span of each.  Box-to-box noise
-is about 3 %, so kernel changes worth 1-2 % are only visible side by side.
+"""Same-box A/B of library builds and runtime settings: alternates `bench.py` runs over the
+given variants and prints the median ms/step, sample span and gather roofline of each.  Box-to-box
+noise is about 3 %, so kernel changes worth 1-2 % are only visible side by side.
 
-    python tools/ab_bench.py --rounds 3 -- scratch/ab/libA.so scratch/ab/libB.so [-- bench args]
+A variant is a libdgs_amd.so path (DGS_AMD_LIB), optionally followed by comma-separated
+environment settings: `ab/u8/libdgs_amd.so,DGS_HUB_BLOCKS=1024`.
+
+    python tools/ab_bench.py --rounds 3 -- ab/a/libdgs_amd.so ab/b/libdgs_amd.so [-- bench args]
 """
 import json
 import os
@@ -11,6 +14,15 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def variant_env(spec):
+    parts = spec.split(",")
+    env = dict(os.environ, DGS_AMD_LIB=os.path.abspath(parts[0]))
+    for kv in parts[1:]:
+        k, v = kv.split("=", 1)
+        env[k] = v
+    return env
 
 
 def main():
@@ -28,9 +40,9 @@ def main():
     res = {lib: [] for lib in libs}
     for r in range(rounds):
         for lib in libs:
-            env = dict(os.environ, DGS_AMD_LIB=os.path.abspath(lib))
             cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline"] + extra
-            out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+            out = subprocess.run(cmd, env=variant_env(lib), capture_output=True, text=True,
+                                 timeout=300)
             if out.returncode != 0:
                 sys.stderr.write(out.stderr[-2000:])
                 sys.exit(out.returncode)
