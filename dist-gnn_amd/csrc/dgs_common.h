@@ -133,8 +133,16 @@ struct Count {
 // ---------------------------------------------------------------------------------
 // Device helpers
 #ifdef __HIPCC__
+// a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96) instead of two v_xor_b32
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 // Philox4x32-10 (curand / Random123 layout).  Each 32x32 product is one 64-bit multiply
-// (v_mad_u64_u32) instead of a mul_lo + mul_hi pair.
+// (v_mad_u64_u32, a quarter-rate instruction: 4.4 v_fma_f32 issue slots measured,
+// tools/valu_bench.hip) instead of a mul_lo + mul_hi pair; each round's two 3-input XORs are one
+// v_bitop3_b32 each.  Round 0 keeps plain XORs: its inputs are often wave-uniform (counter word
+// 0 and the key), and scalar instructions do that round for free.
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -144,8 +152,12 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
     }
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
-    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k.x, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k.y,
-                   (uint32_t)p0);
+    if (r == 0)
+      c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k.x, (uint32_t)p1,
+                     (uint32_t)(p0 >> 32) ^ c.w ^ k.y, (uint32_t)p0);
+    else
+      c = make_uint4(xor3((uint32_t)(p1 >> 32), c.y, k.x), (uint32_t)p1,
+                     xor3((uint32_t)(p0 >> 32), c.w, k.y), (uint32_t)p0);
   }
   return c;
 }

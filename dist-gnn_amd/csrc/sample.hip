@@ -90,8 +90,9 @@ constexpr int kHubShift = 40;
 constexpr uint64_t kHubChunkMask = (uint64_t(1) << kHubShift) - 1;
 constexpr int64_t kHubMaxRows = int64_t(1) << 23;  // hub index field: 24 bits
 struct HubView {
-  // thr[h] (biased hubs): the best k-th A-Res key any worker of hub h has published, in the
-  // order-preserving integer form of key_order()
+  // thr[h]: biased hubs: the best k-th A-Res key any worker of hub h has published, in the
+  // order-preserving integer form of key_order(); uniform hubs: the row's degree (so a worker
+  // moving to the next hub row issues its three loads at once, none dependent on another)
   int64_t *count, *row, *cptr, *hubid, *thr;
   __host__ __device__ static HubView make(int64_t *base, int64_t S) {
     HubView h;
@@ -193,10 +194,12 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
         h = (int64_t)(old >> kHubShift);
         a.hub.row[h] = i;
         a.hub.cptr[h] = (int64_t)(old & kHubChunkMask);
-        if (a.use_hubs == 1)
+        if (a.use_hubs == 1) {
           for (int64_t s2 = 0; s2 < k; ++s2) a.hubslot[i * k + s2] = (int32_t)s2;
-        else
+          a.hub.thr[h] = deg;  // uniform hubs: the row's degree beside its row index
+        } else {
           a.hub.thr[h] = key_order(-__builtin_inff());
+        }
       }
       a.hub.hubid[i] = h;
     }
@@ -281,13 +284,15 @@ __device__ __forceinline__ void emit_slots(const UniformArgs &a, int64_t S, int6
 
 // The 8 draws of one lane in one 512-edge hub chunk (idx = k + 512 q + lane + 64 tt + 128 w)
 // with 32-bit indices: every idx of the chunk is below 2^30.
-template <typename Mod>
+// kFull: the whole chunk lies inside the row (no per-draw bound test).  Each draw keeps its
+// own branch: a wave enters it only when one of its 64 lanes hits (k / idx per lane); one
+// branch over all 8 draws was measured slower (a wave then enters it 8 times as often).
+template <bool kFull, typename Mod>
 __device__ __forceinline__ void hub_chunk32(const uint4 &o4a, const uint4 &o4b, int64_t q,
                                             int64_t k, int64_t deg, int lane, int32_t *sl,
                                             Mod mod) {
   const uint32_t b0 = (uint32_t)(k + 512 * q) + (uint32_t)lane;
   const uint32_t deg32 = (uint32_t)deg, k32 = (uint32_t)k;
-  const bool full = k + 512 * q + 512 <= deg;
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     const uint4 o4 = tt ? o4b : o4a;
@@ -295,7 +300,7 @@ __device__ __forceinline__ void hub_chunk32(const uint4 &o4a, const uint4 &o4b, 
     for (int w = 0; w < 4; ++w) {
       const uint32_t idx = b0 + 64u * tt + 128u * w;
       const uint32_t num = mod(u4_get(o4, w), idx + 1u);
-      if (num < k32 && (full || idx < deg32)) atomicMax(sl + num, (int32_t)idx);
+      if (num < k32 && (kFull || idx < deg32)) atomicMax(sl + num, (int32_t)idx);
     }
   }
 }
@@ -326,7 +331,7 @@ __device__ __forceinline__ void hub_reservoir(const UniformArgs &a, int64_t gw, 
   int32_t *sl = nullptr;
   auto load_row = [&]() {
     r = (int64_t)wave_uniform((uint64_t)hub.row[h]);
-    deg = (int64_t)wave_uniform((uint64_t)ri_deg(a.rowinfo[r]));
+    deg = (int64_t)wave_uniform((uint64_t)hub.thr[h]);
     const uint64_t key = a.seed * (uint64_t)S + (uint64_t)r;
     kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
     sl = a.hubslot + r * k;
@@ -348,14 +353,17 @@ __device__ __forceinline__ void hub_reservoir(const UniformArgs &a, int64_t gw, 
     // is chosen per chunk (wave-uniform test); the 32-bit forms are branch-free up to the (rare)
     // hit, and a chunk entirely inside the row skips the bound test
     const int64_t dmin = k + 512 * q + 1;
-    if (dmin >= (int64_t)kModBigMin && deg < (int64_t(1) << 24))
-      hub_chunk32(o4a, o4b, q, k, deg, lane, sl, mod_big<true>);
+    const bool full = dmin + 511 <= deg;
+    if (full && dmin >= (int64_t)kModBigMin && deg < (int64_t(1) << 24))
+      hub_chunk32<true>(o4a, o4b, q, k, deg, lane, sl, mod_big<true>);
+    else if (dmin >= (int64_t)kModBigMin && deg < (int64_t(1) << 24))
+      hub_chunk32<false>(o4a, o4b, q, k, deg, lane, sl, mod_big<true>);
     else if (dmin >= (int64_t)kModBigMin && deg < (int64_t(1) << 30))
-      hub_chunk32(o4a, o4b, q, k, deg, lane, sl, mod_big<false>);
+      hub_chunk32<false>(o4a, o4b, q, k, deg, lane, sl, mod_big<false>);
     else if (dmin + 511 <= (int64_t)kModMidMax && dmin >= 257)
-      hub_chunk32(o4a, o4b, q, k, deg, lane, sl, mod_mid<true>);
+      hub_chunk32<false>(o4a, o4b, q, k, deg, lane, sl, mod_mid<true>);
     else if (dmin + 511 <= (int64_t)kModMidMax)
-      hub_chunk32(o4a, o4b, q, k, deg, lane, sl, mod_mid<false>);
+      hub_chunk32<false>(o4a, o4b, q, k, deg, lane, sl, mod_mid<false>);
     else {
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
