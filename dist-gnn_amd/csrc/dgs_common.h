@@ -185,9 +185,11 @@ __device__ __forceinline__ uint32_t u4_get(const uint4 &v, int w) {
   return w == 0 ? v.x : (w == 1 ? v.y : (w == 2 ? v.z : v.w));
 }
 
-// curand_uniform(): x * 2^-32 + 2^-33 (exact product, single rounding in the add).
+// curand_uniform(): x * 2^-32 + 2^-33.  The product of the (rounded) float x with a power of
+// two is exact, so the reference's multiply-then-add rounds once, in the add: one fma gives
+// the same bits.
 __device__ __forceinline__ float curand_uniform_from(uint32_t x) {
-  return __fadd_rn(__fmul_rn((float)x, 2.3283064365386963e-10f), 1.1641532182693481e-10f);
+  return __builtin_fmaf((float)x, 2.3283064365386963e-10f, 1.1641532182693481e-10f);
 }
 #endif
 

@@ -90,10 +90,12 @@ constexpr int kHubShift = 40;
 constexpr uint64_t kHubChunkMask = (uint64_t(1) << kHubShift) - 1;
 constexpr int64_t kHubMaxRows = int64_t(1) << 23;  // hub index field: 24 bits
 struct HubView {
-  // thr[h]: biased hubs: the best k-th A-Res key any worker of hub h has published, in the
-  // order-preserving integer form of key_order(); uniform hubs: the row's degree (so a worker
-  // moving to the next hub row issues its three loads at once, none dependent on another)
-  int64_t *count, *row, *cptr, *hubid, *thr;
+  // thr[h] (biased hubs): the best k-th A-Res key any worker of hub h has published, in the
+  // order-preserving integer form of key_order().  aux[h]: what a worker moving to hub row h
+  // needs besides the row index, written by prep so that it is not a load dependent on the
+  // row's node-table entry -- the degree (uniform hubs) or the probability array (biased hubs;
+  // the hub kernel then needs none of the per-location base pointers)
+  int64_t *count, *row, *cptr, *hubid, *thr, *aux;
   __host__ __device__ static HubView make(int64_t *base, int64_t S) {
     HubView h;
     h.count = base;
@@ -101,9 +103,10 @@ struct HubView {
     h.cptr = h.row + S;
     h.hubid = h.cptr + S;
     h.thr = h.hubid + S;
+    h.aux = h.thr + S;
     return h;
   }
-  static size_t bytes(int64_t S) { return sizeof(int64_t) * (size_t)(8 + 4 * S); }
+  static size_t bytes(int64_t S) { return sizeof(int64_t) * (size_t)(8 + 5 * S); }
 };
 
 // Largest h in [0, H) with cptr[h] <= c (cptr nondecreasing, cptr[0] <= c), by a W-ary search:
@@ -196,9 +199,10 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
         a.hub.cptr[h] = (int64_t)(old & kHubChunkMask);
         if (a.use_hubs == 1) {
           for (int64_t s2 = 0; s2 < k; ++s2) a.hubslot[i * k + s2] = (int32_t)s2;
-          a.hub.thr[h] = deg;  // uniform hubs: the row's degree beside its row index
+          a.hub.aux[h] = deg;
         } else {
           a.hub.thr[h] = key_order(-__builtin_inff());
+          a.hub.aux[h] = (int64_t)row_probs(a.src, ri);
         }
       }
       a.hub.hubid[i] = h;
@@ -331,7 +335,7 @@ __device__ __forceinline__ void hub_reservoir(const UniformArgs &a, int64_t gw, 
   int32_t *sl = nullptr;
   auto load_row = [&]() {
     r = (int64_t)wave_uniform((uint64_t)hub.row[h]);
-    deg = (int64_t)wave_uniform((uint64_t)hub.thr[h]);
+    deg = (int64_t)wave_uniform((uint64_t)hub.aux[h]);
     const uint64_t key = a.seed * (uint64_t)S + (uint64_t)r;
     kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
     sl = a.hubslot + r * k;
@@ -529,6 +533,11 @@ __device__ __forceinline__ bool ares_may_pass(float u, float p, float thr) {
   if (!(p > 0.0f)) return false;
   const float bound = p * thr;
   return __builtin_amdgcn_logf(u) >= bound + bound * 0.0000152587890625f - 0.0000152587890625f;
+}
+
+// (a & mask) | (b & ~mask): one v_bfi_b32
+__device__ __forceinline__ uint32_t bitsel(uint32_t mask, uint32_t a, uint32_t b) {
+  return (a & mask) | (b & ~mask);
 }
 
 // number of edges i < d with i = l (mod 32)
@@ -871,7 +880,10 @@ __device__ __forceinline__ int64_t bias_workers(int64_t total, int64_t max_worke
   return w < 1 ? 1 : (w > max_workers ? max_workers : w);
 }
 
-__global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
+#ifndef DGS_BIAS_HUB_WAVES
+#define DGS_BIAS_HUB_WAVES 1
+#endif
+__global__ __launch_bounds__(kTileRows, DGS_BIAS_HUB_WAVES) void k_bias_hub(BiasHubArgs a) {
   const int64_t S = a.Sc.get();
   const int64_t G = (S + 15) / 16;
   const uint64_t packed = (uint64_t)*a.hub.count;
@@ -897,9 +909,8 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
     hstart = a.hub.cptr[hh];
     hnext = hh + 1 < H ? a.hub.cptr[hh + 1] : total;
     const int64_t r = a.hub.row[hh];
-    const RowInfo ri = a.rowinfo[r];
-    deg = ri_deg(ri);
-    pr = row_probs(a.src, ri);
+    deg = ri_deg(a.rowinfo[r]);
+    pr = reinterpret_cast<const float *>(a.hub.aux[hh]);
     const uint64_t key = a.seed * (uint64_t)G + (uint64_t)(r / 16);
     kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
     sub = (uint32_t)(32 * ((r % 16) & 3) + l);
@@ -907,9 +918,33 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
     top = HalfTopK();
     published = key_order(-__builtin_inff());
   };
-  AresPending pend;
+  // Candidates wait in a per-half-wave LDS buffer and are merged into the list 32 at a time:
+  // each insertion costs cross-lane shuffles whose latency the few co-resident waves of this
+  // register-heavy kernel can not hide, so they are paid once per 32 candidates.  The list's
+  // k-th key (the filter) then trails by at most one buffer; anything it lets through is
+  // dropped exactly at the merge.
+  __shared__ float s_ck[kTileRows / 32][64];
+  __shared__ int32_t s_ci[kTileRows / 32][64];
+  const int hw = threadIdx.x >> 5;
+  int ncand = 0;  // buffered candidates of this half-wave (the same on its 32 lanes)
+  auto merge = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    while (ncand > 0) {
+      const int n = ncand < 32 ? ncand : 32;
+      const bool v = l < n;
+      const float ck = v ? s_ck[hw][ncand - n + l] : -__builtin_inff();
+      const int32_t ci = v ? s_ci[hw][ncand - n + l] : INT32_MAX;
+      top.push(ck, ci, v, k, l);
+      ncand -= n;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
   auto flush = [&](int64_t hh) {
-    pend.flush(top, k, l);
+    merge();
     const int64_t slot = wk + hh;
     if (l < top.cnt) {
       a.ckey[slot * k + l] = top.bk;
@@ -938,11 +973,16 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
     const int32_t shared_ord =
         (int32_t)__hip_atomic_load(a.hub.thr + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int64_t i0 = q * kBiasChunk + l;
+    const bool whole = q * kBiasChunk + kBiasChunk <= deg;  // no edge of the chunk past the row
     float p[kT];
 #pragma unroll
     for (int t = 0; t < kT; ++t) {
       const int64_t i = i0 + 32 * t;
-      p[t] = pr[i < deg ? i : deg - 1];
+#ifdef DGS_EXP_NOPROBS
+      p[t] = 1.0f + (float)(i & 7);
+#else
+      p[t] = pr[whole || i < deg ? i : deg - 1];
+#endif
     }
     // this lane's 16 draws j = jb + 16q + t lie in 5 consecutive Philox blocks (uniform
     // control flow -- lanes' chain offsets differ, a lazy per-lane refill would diverge into a
@@ -974,18 +1014,60 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub(BiasHubArgs a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) carry[e] = wv[4 * (kT / 4) + e];
     carry_cb = cb + kT / 4;
+    // draw t = word off + t, selected in two steps (off & 2, then off & 1) with bit-select
+    // masks (a select on the offset bit would be folded into a dynamically indexed array)
+    const uint32_t m2 = (off & 2) ? ~0u : 0u, m1 = (off & 1) ? ~0u : 0u;
+    uint32_t w2[kT + 1];
+#pragma unroll
+    for (int e = 0; e < kT + 1; ++e) w2[e] = bitsel(m2, wv[e + 2], wv[e]);
+    // The chunk's filter threshold, fixed for its 16 steps: this worker's k-th key once its list
+    // is full, or the best k-th any worker of the row has published -- both lower bounds of the
+    // row's final k-th key, so an edge the cheap test rejects can not be among the row's picks.
+    bool filter = top.filtering(k) || shared_ord != published_none;
+    float thr = key_from_order(top.filtering(k) ? max(key_order(top.thr_k), shared_ord)
+                                                : shared_ord);
+    float u[kT];
+    uint32_t m = 0;  // bit t: edge i0 + 32 t is a candidate
 #pragma unroll
     for (int t = 0; t < kT; ++t) {
-      const int64_t i = i0 + 32 * t;
-      uint32_t x = wv[t];
-      x = off == 1 ? wv[t + 1] : x;
-      x = off == 2 ? wv[t + 2] : x;
-      x = off == 3 ? wv[t + 3] : x;
-      const float u = curand_uniform_from(x);
-      const bool own = top.filtering(k);
-      const int32_t ord = own ? max(key_order(top.thr_k), shared_ord) : shared_ord;
-      pend.add(u, p[t], i, i < deg, top, k, l, own || shared_ord != published_none,
-               key_from_order(ord));
+      u[t] = curand_uniform_from(bitsel(m1, w2[t + 1], w2[t]));
+      const bool valid = whole || i0 + 32 * t < deg;
+      m |= (uint32_t)(valid && (!filter || ares_may_pass(u[t], p[t], thr))) << t;
+    }
+    // Candidates go into the top-k list in rounds of one per lane (each round one sorted
+    // merge, or one-by-one insertion when few lanes have one); the resulting list does not
+    // depend on the order.  Unfiltered (the worker's first steps in a row), the rest of the
+    // candidates are re-tested once the first round has filled the list.
+    while (half_ballot(m != 0)) {
+      const bool has = m != 0;
+      const int t = has ? __builtin_ctz(m) : 0;
+      m &= m - 1;
+      float ut = u[0], pt = p[0];
+#pragma unroll
+      for (int e = 1; e < kT; ++e) {
+        ut = t == e ? u[e] : ut;
+        pt = t == e ? p[e] : pt;
+      }
+      const float key = has ? ares_key(ut, pt) : -__builtin_inff();
+      const int32_t it = (int32_t)(i0 + 32 * t);
+      const bool keep = has && ares_better(key, it, top.thr_k, top.thr_i);
+      const uint32_t b = half_ballot(keep);
+      if (keep) {
+        const int pos = ncand + __builtin_popcount(b & ((1u << l) - 1u));
+        s_ck[hw][pos] = key;
+        s_ci[hw][pos] = it;
+      }
+      ncand += __builtin_popcount(b);
+      if (ncand >= 32) merge();
+      if (!filter && top.filtering(k)) {
+        filter = true;
+        thr = top.thr_k;
+        uint32_t keep = 0;
+#pragma unroll
+        for (int e = 0; e < kT; ++e)
+          keep |= (uint32_t)ares_may_pass(u[e], p[e], thr) << e;
+        m &= keep;
+      }
     }
     // publish this worker's k-th key when it improved on what it last published
     if (top.filtering(k)) {

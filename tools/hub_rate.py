@@ -27,7 +27,12 @@ def run(args):
     indptr_d, indices_d = rmat_csc_torch(args.scale, args.ef, seed=20261015, device=dev)
     deg = (indptr_d[1:] - indptr_d[:-1])
     N = deg.numel()
-    sampler = dgs.classes.P2PCacheSampler(indptr_d.cpu(), indices_d.cpu(), torch.Tensor(),
+    probs = torch.Tensor()
+    if args.bias:  # bench.py --bias: degree-weighted
+        indeg = torch.bincount(indices_d, minlength=N)
+        probs = (1 + indeg[indices_d]).to(torch.float32).cpu()
+        del indeg
+    sampler = dgs.classes.P2PCacheSampler(indptr_d.cpu(), indices_d.cpu(), probs,
                                           torch.arange(N), 0)
     fan_out = [int(x) for x in args.fan_out.split(",")]
     g = torch.Generator().manual_seed(2)
@@ -40,8 +45,11 @@ def run(args):
         for h, (seeds, _, _, _) in enumerate(blocks):
             k = fan_out[len(fan_out) - 1 - h]
             d = deg[seeds]
-            hub = d - k > 128
-            per_hop[h].append({"draws": int((d[hub] - k).sum()), "hub_rows": int(hub.sum()),
+            # uniform: reservoir draws of rows with deg - k > 128; biased: every edge of the rows
+            # with deg > 1024 (one key each)
+            hub = d > 1024 if args.bias else d - k > 128
+            draws = int(d[hub].sum()) if args.bias else int((d[hub] - k).sum())
+            per_hop[h].append({"draws": draws, "hub_rows": int(hub.sum()),
                                "rows": int(seeds.numel()),
                                "max_deg": int(d.max()) if d.numel() else 0})
     torch.cuda.synchronize()
@@ -61,13 +69,16 @@ def synthetic(args):
     D, rows = args.synthetic_hub, args.rows
     indptr = torch.tensor([0, D], dtype=torch.int64)
     indices = torch.zeros(D, dtype=torch.int64)
-    sampler = dgs.classes.P2PCacheSampler(indptr, indices, torch.Tensor(), torch.arange(1), 0)
+    probs = torch.rand(D, generator=torch.Generator().manual_seed(1)) + 0.01 if args.bias \
+        else torch.Tensor()
+    sampler = dgs.classes.P2PCacheSampler(indptr, indices, probs, torch.arange(1), 0)
     k = int(args.fan_out.split(",")[-1])
     s = torch.zeros(rows, dtype=torch.int64, device="cuda")
     per_hop = [[]]
     for c in range(args.calls):
         sampler._CAPI_sample_node_classifiction(s, [k], False)
-        per_hop[0].append({"draws": rows * (D - k), "hub_rows": rows, "rows": rows,
+        per_hop[0].append({"draws": rows * (D if args.bias else D - k), "hub_rows": rows,
+                           "rows": rows,
                            "max_deg": D})
     torch.cuda.synchronize()
     json.dump({"fan_out": [k], "per_hop": per_hop}, open(args.out, "w"))
@@ -78,7 +89,7 @@ def report(args):
     L = len(d["fan_out"])
     durs = []
     for r in csv.DictReader(open(args.trace)):
-        if "k_hub_reservoir" in r["Kernel_Name"]:
+        if args.kernel in r["Kernel_Name"]:
             durs.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
     durs = [x[1] for x in sorted(durs)]
     calls = len(d["per_hop"][0])
@@ -102,6 +113,9 @@ if __name__ == "__main__":
     p.add_argument("--report")
     p.add_argument("--trace")
     p.add_argument("--synthetic-hub", type=int, default=0)
+    p.add_argument("--bias", action="store_true")
+    p.add_argument("--kernel", default="k_hub_reservoir",
+                   help="kernel whose launches --report prices (k_bias_hub for --bias)")
     p.add_argument("--rows", type=int, default=1)
     a = p.parse_args()
     report(a) if a.report else (synthetic(a) if a.synthetic_hub else run(a))
