@@ -668,41 +668,6 @@ struct HalfTopK {
   }
 };
 
-// A-Res candidates waiting to be merged: up to two per lane (u, p, edge).  An edge that passes
-// the cheap test is parked; the exact keys are computed and merged in one batch when some lane
-// would hold a third, or at the end -- so a merge absorbs many candidates instead of running
-// for every step with one.
-struct AresPending {
-  float u0 = 0.0f, p0 = 0.0f, u1 = 0.0f, p1 = 0.0f;
-  int32_t i0 = 0, i1 = 0;
-  bool h0 = false, h1 = false;
-  __device__ __forceinline__ void flush(HalfTopK &top, int64_t k, int l) {
-    if (half_ballot(h0)) top.push(h0 ? ares_key(u0, p0) : -__builtin_inff(), i0, h0, k, l);
-    if (half_ballot(h1)) top.push(h1 ? ares_key(u1, p1) : -__builtin_inff(), i1, h1, k, l);
-    h0 = h1 = false;
-  }
-  // edge i (valid) with draw u and weight p; `filter`: thr is a lower bound of the final k-th
-  // key (the list's own k-th, or a bound another worker of the row published)
-  __device__ __forceinline__ void add(float u, float p, int64_t i, bool valid, HalfTopK &top,
-                                      int64_t k, int l, bool filter, float thr) {
-    const bool cand = valid && (!filter || ares_may_pass(u, p, thr));
-    if (half_ballot(cand && h0 && h1)) flush(top, k, l);
-    if (cand) {
-      if (!h0) {
-        u0 = u;
-        p0 = p;
-        i0 = (int32_t)i;
-        h0 = true;
-      } else {
-        u1 = u;
-        p1 = p;
-        i1 = (int32_t)i;
-        h1 = true;
-      }
-    }
-  }
-};
-
 template <bool kReplace>
 __global__ __launch_bounds__(kTileRows) void k_sample_bias(
     RowSrc src, Count Sc, int64_t k, uint64_t seed, const RowInfo *__restrict__ rowinfo,
@@ -750,26 +715,73 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
       }
       if (hubid && hubid[r] >= 0) return;  // split across half-waves: k_bias_hub / _merge
       HalfTopK top;
-      uint4 o4 = make_uint4(0, 0, 0, 0);
-      int64_t cached_q = -1;
-      AresPending pend;
-      for (int64_t base = 0; base < deg; base += 32) {
-        const int64_t i = base + l;
-        float u = 0.0f, pv = 0.0f;
-        if (i < deg) {
-          const int64_t q = j >> 2;
-          if (q != cached_q) {
-            o4 = philox4x32_10(make_uint4((uint32_t)q, (uint32_t)((uint64_t)q >> 32), sub, 0u),
-                               kk);
-            cached_q = q;
-          }
-          u = curand_uniform_from(u4_get(o4, (int)(j & 3)));
-          pv = pr[i];
-          ++j;
-        }
-        pend.add(u, pv, i, i < deg, top, k, l, top.filtering(k), top.thr_k);
+      // Step s of this lane (edge i = 32 s + l) uses draw j + s.  Steps go in groups of 4
+      // over a window of two Philox blocks, one new block per group for every lane alike (the
+      // lanes' offsets inside a block differ, so a per-lane lazy refill would diverge into a
+      // block per step); the draw is picked with bit-select masks on the offset.
+      const int64_t bl = j >> 2;
+      const int off = (int)(j & 3);
+      const uint32_t m2 = (off & 2) ? ~0u : 0u, m1 = (off & 1) ? ~0u : 0u;
+      uint4 A = philox4x32_10(make_uint4((uint32_t)bl, (uint32_t)((uint64_t)bl >> 32), sub, 0u), kk);
+      bool filter = false;
+      float thr = -__builtin_inff();
+      const int64_t nsteps = (deg + 31) / 32;
+      float pn[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int64_t i = 32 * s4 + l;
+        pn[s4] = i < deg ? pr[i] : 0.0f;
       }
-      pend.flush(top, k, l);
+      for (int64_t g = 0; 4 * g < nsteps; ++g) {
+        float p[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          p[s4] = pn[s4];
+          const int64_t i = 128 * (g + 1) + 32 * s4 + l;  // the next group's loads go out now
+          pn[s4] = i < deg ? pr[i] : 0.0f;
+        }
+        const uint64_t qb = (uint64_t)(bl + g + 1);
+        const uint4 B = philox4x32_10(make_uint4((uint32_t)qb, (uint32_t)(qb >> 32), sub, 0u), kk);
+        const uint32_t wv[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+        uint32_t w2[5];
+#pragma unroll
+        for (int e = 0; e < 5; ++e) w2[e] = bitsel(m2, wv[e + 2], wv[e]);
+        float u[4];
+        uint32_t mk = 0;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          u[s4] = curand_uniform_from(bitsel(m1, w2[s4 + 1], w2[s4]));
+          const bool valid = 128 * g + 32 * s4 + l < deg;
+          mk |= (uint32_t)(valid && (!filter || ares_may_pass(u[s4], p[s4], thr))) << s4;
+        }
+        // candidates in rounds of one per lane (the resulting list does not depend on order)
+        while (half_ballot(mk != 0)) {
+          const bool has = mk != 0;
+          const int t = has ? __builtin_ctz(mk) : 0;
+          mk &= mk - 1;
+          float ut = u[0], pt = p[0];
+#pragma unroll
+          for (int e = 1; e < 4; ++e) {
+            ut = t == e ? u[e] : ut;
+            pt = t == e ? p[e] : pt;
+          }
+          top.push(has ? ares_key(ut, pt) : -__builtin_inff(), (int32_t)(128 * g + 32 * t + l),
+                   has, k, l);
+          if (!filter && top.filtering(k)) {
+            filter = true;
+            thr = top.thr_k;
+            uint32_t keep = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) keep |= (uint32_t)ares_may_pass(u[e], p[e], thr) << e;
+            mk &= keep;
+          }
+        }
+        if (top.filtering(k)) {
+          filter = true;
+          thr = top.thr_k;
+        }
+        A = B;
+      }
       if (l < k) {
         const int64_t v = nb[top.bi];
         rowpos[out + l] = r;
