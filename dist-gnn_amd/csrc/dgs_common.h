@@ -133,6 +133,17 @@ struct Count {
 // ---------------------------------------------------------------------------------
 // Device helpers
 #ifdef __HIPCC__
+// Global-address-space view of a pointer that came from memory (a node-table entry, a hub
+// record): loads through it are global_load, not flat_load.  Flat loads count on lgkmcnt as
+// well as vmcnt and complete out of order, so every LDS / shuffle / scalar-load wait would also
+// wait for them and no wait could be counted.
+template <typename T>
+using global_ptr = const __attribute__((address_space(1))) T *;
+template <typename T>
+__device__ __forceinline__ global_ptr<T> as_global(const T *p) {
+  return (global_ptr<T>)(uintptr_t)p;
+}
+
 // a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96) instead of two v_xor_b32
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);

@@ -30,7 +30,10 @@ constexpr int kGroup = 16;       // lanes per row in the uniform kernel
 constexpr int kRowsPerBlock = kTileRows / kGroup;  // rows per uniform-sampling workgroup
 constexpr int kHubT = 128;       // reservoir tail length above which a row goes to the hub kernel
 constexpr int kBiasHubT = 1024;  // biased rows above this degree are split across half-waves
-constexpr int kBiasChunk = 512;  // edges per biased hub chunk (32 lanes x 16 draws)
+#ifndef DGS_BIAS_CHUNK
+#define DGS_BIAS_CHUNK 256
+#endif
+constexpr int kBiasChunk = DGS_BIAS_CHUNK;  // edges per biased hub chunk (32 lanes x 8 draws)
 constexpr int kBiasHubBlocks = 1024;  // workgroups of the biased hub kernel (8 half-waves each)
 constexpr int kHubBlocks = 1536; // workgroups of the hub kernel: 6 of 8 waves per SIMD, so the
                                  // other batches in flight (feature gather) find free slots
@@ -276,7 +279,7 @@ struct UniformArgs {
 
 // Writes the k picks of row r whose reservoir slots are `slots` (16-lane group, lane L).
 __device__ __forceinline__ void emit_slots(const UniformArgs &a, int64_t S, int64_t r,
-                                           const int64_t *nb, int64_t out,
+                                           global_ptr<int64_t> nb, int64_t out,
                                            const int32_t *slots, int L) {
   for (int64_t s2 = L; s2 < a.k; s2 += kGroup) {
     const int64_t v = nb[slots[s2]];
@@ -399,7 +402,7 @@ __device__ __forceinline__ void sample_rows(const UniformArgs &a, int64_t blk, i
   int32_t *sl = s_slot + g * k;
   const RowInfo ri = a.rowinfo[r];
   const int64_t deg = ri_deg(ri);
-  const int64_t *nb = ri.ptr;
+  const global_ptr<int64_t> nb = as_global(ri.ptr);
   const int64_t out = a.boff[r / kTileRows] + a.tpre[r];
   const uint64_t key = a.seed * (uint64_t)S + (uint64_t)r;
   const uint2 kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
@@ -684,8 +687,8 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
     if (r >= S) return;
     const RowInfo ri = rowinfo[r];
     const int64_t deg = ri_deg(ri);
-    const int64_t *nb = ri.ptr;
-    const float *pr = row_probs(src, ri);
+    const global_ptr<int64_t> nb = as_global(ri.ptr);
+    const global_ptr<float> pr = as_global(row_probs(src, ri));
     const int64_t out = boff[r / kTileRows] + tpre[r];
     // reference coordinates: block b = r / 16, warp w = (r % 16) % 4, chain position m
     const int64_t b = r / 16;
@@ -912,7 +915,7 @@ __global__ __launch_bounds__(kTileRows, DGS_BIAS_HUB_WAVES) void k_bias_hub(Bias
   const int64_t k = a.k;
   int64_t h = group_search<32>(a.hub.cptr, H, c0);  // largest h with cptr[h] <= c0
   int64_t hstart = 0, hnext = 0, deg = 0, jb = 0;
-  const float *pr = nullptr;
+  global_ptr<float> pr = nullptr;
   int32_t published = key_order(-__builtin_inff());
   uint2 kk;
   uint32_t sub = 0;
@@ -922,7 +925,7 @@ __global__ __launch_bounds__(kTileRows, DGS_BIAS_HUB_WAVES) void k_bias_hub(Bias
     hnext = hh + 1 < H ? a.hub.cptr[hh + 1] : total;
     const int64_t r = a.hub.row[hh];
     deg = ri_deg(a.rowinfo[r]);
-    pr = reinterpret_cast<const float *>(a.hub.aux[hh]);
+    pr = as_global(reinterpret_cast<const float *>(a.hub.aux[hh]));
     const uint64_t key = a.seed * (uint64_t)G + (uint64_t)(r / 16);
     kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
     sub = (uint32_t)(32 * ((r % 16) & 3) + l);
@@ -982,6 +985,8 @@ __global__ __launch_bounds__(kTileRows, DGS_BIAS_HUB_WAVES) void k_bias_hub(Bias
     if (l == 0 && c == hnext - 1) a.wlast[h] = (int32_t)wk;
     // Every worker's k-th key bounds the row's final k-th key from below, so the best one
     // published so far filters this worker's edges too (stale reads only filter less).
+    // (Loading it and the probabilities one chunk ahead costs more registers than the latency
+    // it hides: 3 instead of 4 waves per SIMD, -20 %.)
     const int32_t shared_ord =
         (int32_t)__hip_atomic_load(a.hub.thr + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int64_t i0 = q * kBiasChunk + l;
@@ -990,16 +995,12 @@ __global__ __launch_bounds__(kTileRows, DGS_BIAS_HUB_WAVES) void k_bias_hub(Bias
 #pragma unroll
     for (int t = 0; t < kT; ++t) {
       const int64_t i = i0 + 32 * t;
-#ifdef DGS_EXP_NOPROBS
-      p[t] = 1.0f + (float)(i & 7);
-#else
       p[t] = pr[whole || i < deg ? i : deg - 1];
-#endif
     }
-    // this lane's 16 draws j = jb + 16q + t lie in 5 consecutive Philox blocks (uniform
-    // control flow -- lanes' chain offsets differ, a lazy per-lane refill would diverge into a
-    // Philox per step); select draw t as word off + t.  The first block was the previous
-    // chunk's last whenever the worker stays in the row, so 4 are computed.
+    // this lane's kT draws j = jb + kT q + t lie in kT / 4 + 1 consecutive Philox blocks
+    // (uniform control flow -- lanes' chain offsets differ, a lazy per-lane refill would diverge
+    // into a Philox per step); select draw t as word off + t.  The first block was the previous
+    // chunk's last whenever the worker stays in the row, so kT / 4 are computed.
     const int64_t j0 = jb + q * kT;
     const int64_t cb = j0 >> 2;
     const int off = (int)(j0 & 3);
@@ -1160,7 +1161,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
       const RowInfo ri = a.rowinfo[r];
       const int64_t out = a.boff[r / kTileRows] + a.tpre[r];
       if (l < k) {
-        const int64_t v = ri.ptr[s_idx[0][l]];
+        const int64_t v = as_global(ri.ptr)[s_idx[0][l]];
         a.rowpos[out + l] = r;
         a.col[out + l] = v;
         table_record(a.table, v, S + out + l);
