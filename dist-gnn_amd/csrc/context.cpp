@@ -200,9 +200,10 @@ struct StampRec {
   bool own;  // a separate allocation (slab full), returned to the pool at collect
 };
 // Workgroup stamps are bump-allocated from one slab reserved when profiling is switched on,
-// so a profiled launch inside a timed region never calls hipMalloc.  256 MB holds 2 x 8 B
-// for 16 M workgroups (B = 1024: ~5000 gathers; B = 8192: ~600) before falling back.
-constexpr int64_t kStampSlabWords = int64_t(32) << 20;
+// so a profiled launch inside a timed region never calls hipMalloc.  1 GiB holds 2 x 8 B for
+// 64 M workgroups (one-wave gather workgroups: B = 1024 ~5000 gathers, B = 8192 ~2100) before
+// falling back.
+constexpr int64_t kStampSlabWords = int64_t(128) << 20;
 struct StampSlab {
   uint64_t *base = nullptr;
   int64_t used = 0;
