@@ -17,7 +17,7 @@ S=$(find $O/stats -name '*kernel_stats.csv' | head -n 1)
 T=$(find $O/stats -name '*kernel_trace.csv' | head -n 1)
 cp "$S" $P/${R}_bench_kernel_stats.csv
 python tools/prof_summary.py "$S" 40 > $P/${R}_bench_kernel_stats_summary.txt
-python tools/timeline.py "$T" > $P/${R}_timeline_uniform.txt
+python tools/timeline.py "$T" --warmup 30 --steps 1000 > $P/${R}_timeline_uniform.txt
 if [ -d $O/stats_bias ]; then
   python tools/timeline.py "$(find $O/stats_bias -name '*kernel_trace.csv' | head -n 1)" \
     > $P/${R}_timeline_bias_sequential.txt
