@@ -185,28 +185,26 @@ def main():
     # only the gather kernel is measured in the timed region: its workgroups stamp their own
     # start / end (no stream markers between the measured kernels)
     dgs.ops.profile_enable(dgs.ops.PROFILE_GATHER)
+    seg0 = torch.cuda.memory_stats(dev).get("segment.all.allocated", 0)
     edges = rows = 0
     t0 = time.perf_counter()
-    last_nids = []
     step_t = []
     for blocks, x, _ in it:
         step_t.append(time.perf_counter())
         edges += sum(b[2].numel() for b in blocks)
         rows += x.shape[0]
-        if len(last_nids) < 20:
-            last_nids.append(blocks[-1][1])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     prof = dgs.ops.profile_read()
+    # hipMalloc calls the caching allocator made inside the timed region (host stalls)
+    mallocs = torch.cuda.memory_stats(dev).get("segment.all.allocated", 0) - seg0
     # host-side spacing of consecutive batches handed out by the loader (jitter diagnostics)
     gaps = np.diff(np.array([t0] + step_t)) * 1e3
     step_gaps = {"p10": float(np.percentile(gaps, 10)), "p50": float(np.median(gaps)),
                  "p90": float(np.percentile(gaps, 90)), "max": float(gaps.max())}
-    host_rows = sum(float((~cached_mask[n.long()]).sum()) / max(n.numel(), 1)
-                    for n in last_nids) / max(len(last_nids), 1)
     # informational, outside the timed region: the sequential loop's latency per sample call
     # (host wall, sample + label select), its GPU span, and the feature gather on its own
     n_side = min(args.steps, 20)
@@ -221,6 +219,11 @@ def main():
     torch.cuda.synchronize()
     seq_ms = (time.perf_counter() - ts) * 1e3 / n_side
     side = dgs.ops.profile_read()
+    # share of the gathered rows that are host rows, over the side pass's batches (the timed
+    # loop keeps no batch alive: each one it held would pin its output buffers, and the
+    # caching allocator would hipMalloc fresh ones inside the timed region)
+    host_rows = sum(float((~cached_mask[n.long()]).sum()) / max(n.numel(), 1)
+                    for n in side_nids) / max(len(side_nids), 1)
     dgs.ops.profile_enable(dgs.ops.PROFILE_GATHER)
     iso_rows = 0
     for n in side_nids:
@@ -282,6 +285,7 @@ def main():
             "pipeline_depth": args.depth,
         },
         "host_step_gap_ms": step_gaps,
+        "allocator_mallocs_in_timed_region": mallocs,
         "host_row_share": host_rows,
         # host rows cross PCIe Gen5 x16 (63 GB/s spec): their read rate during the gather
         "gather_host_read_GBps": (host_rows * rows * row_bytes / (prof["gather_ms"] * 1e-3) / 1e9
