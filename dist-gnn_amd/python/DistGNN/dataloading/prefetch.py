@@ -54,7 +54,7 @@ class PrefetchLoader:
     Up to `depth` batches are in flight, batch i on the loader's stream i mod depth (streams
     are the loader's own until close()).  Every tensor handed out is ready on the caller's
     current stream when __next__ returns (that stream waits for the batch's stream; the host
-    does not block on it); the feature gather itself runs on the caller's stream.  Each
+    does not block on it); the feature and label gathers run on the caller's stream.  Each
     batch's per-hop launch seeds are drawn from the global engine by the sampler when it
     accepts the call, in batch order, so the output is exactly that of the sequential loop
     after the same dgs.ops._CAPI_set_random_seed (several live loaders draw in the order
@@ -104,19 +104,12 @@ class PrefetchLoader:
         # the caller may drop its seeds at once: their memory must outlive B's reads
         seeds.record_stream(self._streams[w])
         prep = self.sampler._prepare(seeds, self.fan_out)  # int64 seeds + outputs, on C
-        s64 = prep[0]
-        y = None
-        if self.labels is not None:
-            y = torch.empty((s64.numel(),) + tuple(self.labels.shape[1:]),
-                            dtype=self.labels.dtype, device=self.device)
         dgs.ops._stream_wait(cur, st)
-        if y is not None:  # depends on the seeds only: issued first
-            dgs.ops._index_select_into(self.labels, s64, y, st)
         # B is not touched again before result(): the sampler's launcher thread may issue
         # the launches.  The sampler draws the launch seeds once it has accepted the call.
         pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, _HOST_ASYNC,
                                                st)
-        self._inflight.append((pending, y, w))
+        self._inflight.append((pending, prep[0], w))
 
     def __iter__(self):
         return self
@@ -127,7 +120,7 @@ class PrefetchLoader:
         if not self._inflight:
             self.close()  # returns the streams
             raise StopIteration
-        pending, y, w = self._inflight.popleft()
+        pending, s64, w = self._inflight.popleft()
         st = self._st[w]
         cur = self._caller_stream()
         try:
@@ -136,14 +129,23 @@ class PrefetchLoader:
             dgs.ops._stream_wait(st, cur)
             self.close()
             raise
-        # C after B (the sample call, the label gather); the feature gather then runs on C,
-        # whose hardware queue the batch streams do not use
+        # C after B (the sample call); the feature and label gathers then run on C, whose
+        # hardware queue the batch streams do not use
         dgs.ops._stream_wait(st, cur)
         x = None
         if self.server is not None:
             front = blocks[-1][1]
             x = self.server._get_feature_alloc(front)
             self.server._get_feature_into(front, x, cur)
+        y = None
+        if self.labels is not None:
+            # the label gather depends on the seeds only; on C it stays off the batch's
+            # critical path (issued on B in front of the sample call, it delayed hop 0 while
+            # it waited for a slot on CUs the other batches fill: a 20-step run's first batch
+            # came 0.17 ms later, 2.43-2.50 -> 2.59-2.68 G edges/s over 5 same-box runs)
+            y = torch.empty((s64.numel(),) + tuple(self.labels.shape[1:]),
+                            dtype=self.labels.dtype, device=self.device)
+            dgs.ops._index_select_into(self.labels, s64, y, cur)
         dt = self.sampler._id_dtype
         if dt != torch.int64:  # int32 graphs: cast on the caller's stream, now ordered after B
             cast, cur_seeds = [], blocks[0][0]
