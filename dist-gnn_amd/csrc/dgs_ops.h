@@ -102,7 +102,7 @@ Table relabel_table(HopScratch &ws, int64_t n_ub, hipStream_t st);
 // Direct-layout table over node ids [0, num_nodes) (val = empty everywhere on return; a table
 // left dirty by an interrupted hop is re-filled).  The relabel pass of every hop empties the
 // entries it touched, so a completed hop leaves it clean.
-Table direct_table(DevBuf &val, DevBuf &lab, int64_t num_nodes, bool *dirty, hipStream_t st);
+Table direct_table(DevBuf &pairs, int64_t num_nodes, bool *dirty, hipStream_t st);
 
 // Relabel for the node-classification hop: mapping = cat(seeds[S], col[nnz]) where nnz is
 // read from d_nnz (device); writes unique ids to `unique` (first-occurrence order),

@@ -12,12 +12,14 @@ constexpr int32_t kTableNoPos = 0x7FFFFFFF;
 
 // Two layouts.  Hashed (key != nullptr): open addressing over arbitrary int64 ids (the
 // standalone relabel op).  Direct (direct == true): the sampler's ids are graph node ids in
-// [0, N), so val / lab are indexed by the id itself -- one load and at most one atomicMin per
-// insert, no probing, no key CAS and no slot_of bookkeeping (2 x 4 bytes of HBM per node).
+// [0, N), so the entry is indexed by the id itself -- one load and at most one atomicMin per
+// insert, no probing, no key CAS and no slot_of bookkeeping.  A node's (val, lab) pair is one
+// 8-byte word (val at 2x, lab at 2x + 1 of `val`): the scatter's val read and lab write, and
+// the relabel tail's lab read and val reset, touch one cache line per node instead of two.
 struct Table {
   int64_t *key;   // hashed layout: slot keys; nullptr with !direct: no table (standalone op)
-  int32_t *val;   // minimum position (first occurrence), per slot or per node
-  int32_t *lab;   // label = rank among first occurrences, per slot or per node
+  int32_t *val;   // minimum position (first occurrence), per slot; direct: the pair array
+  int32_t *lab;   // label = rank among first occurrences, per slot; direct: unused
   uint32_t *slot_of;  // hashed layout: slot of every inserted position
   uint64_t mask;  // hashed layout: capacity - 1
   bool direct;
@@ -41,19 +43,23 @@ struct RelabelTail {
 };
 
 #ifdef __HIPCC__
+// direct layout: node x's first position and label
+__device__ __forceinline__ int32_t *dval(const Table &t, int64_t x) { return t.val + 2 * x; }
+__device__ __forceinline__ int32_t *dlab(const Table &t, int64_t x) { return t.val + 2 * x + 1; }
+
 __device__ __forceinline__ void relabel_tail_block(const RelabelTail &r, int64_t blk) {
   const int64_t na = r.Sc.get();
   const int64_t nb = *r.d_nb;
   const int64_t e = blk * 256 + threadIdx.x;
   if (e < nb) {
     const int64_t v = r.out_col[e];
-    r.out_col[e] = r.t.lab[v];
-    if (r.remap_rows) r.out_row[e] = r.t.lab[r.seeds[r.out_row[e]]];
-    r.t.val[v] = kTableNoPos;
+    r.out_col[e] = *dlab(r.t, v);
+    if (r.remap_rows) r.out_row[e] = *dlab(r.t, r.seeds[r.out_row[e]]);
+    *dval(r.t, v) = kTableNoPos;
   }
   if (e < na) {
     const int64_t s = r.seeds[e];
-    if ((uint64_t)s < (uint64_t)r.t.n) r.t.val[s] = kTableNoPos;
+    if ((uint64_t)s < (uint64_t)r.t.n) *dval(r.t, s) = kTableNoPos;
   }
 }
 
@@ -91,7 +97,8 @@ __device__ __forceinline__ void table_record(const Table &t, int64_t x, int64_t 
     // val only decreases: skip the atomic when an earlier occurrence is already recorded.  (A
     // no-return atomic without the check measured 1.8x slower on the last hop: hot nodes
     // recur ~1000 times per hop and same-address atomics serialise.)
-    if (t.val[x] > (int32_t)pos) atomicMin(t.val + x, (int32_t)pos);
+    int32_t *v = dval(t, x);
+    if (*v > (int32_t)pos) atomicMin(v, (int32_t)pos);
   } else if (t.key) {
     t.slot_of[pos] = table_insert(t, x, (int32_t)pos);
   }

@@ -141,7 +141,7 @@ __device__ __forceinline__ int64_t first_flags(const int64_t *a, int64_t na, con
   }
 #pragma unroll
   for (int j = 0; j < kCompactItems; ++j)
-    pv[j] = (uint64_t)x[j] < (uint64_t)t.n ? t.val[x[j]] : kNoPos;
+    pv[j] = (uint64_t)x[j] < (uint64_t)t.n ? *dval(t, x[j]) : kNoPos;
   int64_t cnt = 0;
 #pragma unroll
   for (int j = 0; j < kCompactItems; ++j) {
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(kThreads) void k_dscatter(const int64_t *a, Count n
   for (int j = 0; j < kCompactItems; ++j) {
     if (f[j]) {
       unique[ex] = x[j];
-      t.lab[x[j]] = (int32_t)ex;
+      *dlab(t, x[j]) = (int32_t)ex;
       ++ex;
     }
   }
@@ -267,17 +267,16 @@ void launch_relabel_tail(const RelabelTail &tail, hipStream_t st) {
   DGS_LAUNCH_CHECK();
 }
 
-Table direct_table(DevBuf &val, DevBuf &lab, int64_t num_nodes, bool *dirty, hipStream_t st) {
-  const int64_t n = num_nodes > 0 ? num_nodes : 1;
-  const bool fresh = val.ensure(sizeof(int32_t) * (size_t)n);
-  lab.ensure(sizeof(int32_t) * (size_t)n);
+Table direct_table(DevBuf &pairs, int64_t num_nodes, bool *dirty, hipStream_t st) {
+  const int64_t n = 2 * (num_nodes > 0 ? num_nodes : 1);  // (val, lab) per node
+  const bool fresh = pairs.ensure(sizeof(int32_t) * (size_t)n);
   if (fresh || *dirty) {
     hipLaunchKernelGGL(k_fill_i32, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st,
-                       val.as<int32_t>(), n, kNoPos);
+                       pairs.as<int32_t>(), n, kNoPos);
     DGS_LAUNCH_CHECK();
     *dirty = false;
   }
-  return Table{nullptr, val.as<int32_t>(), lab.as<int32_t>(), nullptr, 0, true, num_nodes};
+  return Table{nullptr, pairs.as<int32_t>(), nullptr, nullptr, 0, true, num_nodes};
 }
 
 // The hop's seeds and sampled neighbours were already inserted by the sampling kernels

@@ -347,7 +347,7 @@ void Sampler::launch(Ctx &c, const Job &j, hipStream_t st) {
     int64_t *d_nnz = dsz + 3 * h + 2;
     int64_t *d_uniq = dsz + 3 * h + 1;
     const int tb = h & 1;
-    const Table t = direct_table(c.dval[tb], c.dlab[tb], num_nodes_, &c.dirty[tb], st);
+    const Table t = direct_table(c.dpair[tb], num_nodes_, &c.dirty[tb], st);
     c.dirty[tb] = true;
     // rows[h] receives each edge's seed row r from the sampler and is relabelled in place
     sample_hop(src, cur, S, k, replace, bias_, seed, rows[h], cols[h], d_nnz, t, c.ws, st,

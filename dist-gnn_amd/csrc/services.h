@@ -116,7 +116,7 @@ class Sampler {
     bool job_ready = false, job_done = true, stop = false;
     std::exception_ptr job_err;
     HopScratch ws;
-    DevBuf dval[2], dlab[2];  // direct relabel tables over node ids (first position, label),
+    DevBuf dpair[2];  // direct relabel tables over node ids ((first position, label) pairs),
     bool dirty[2] = {false, false};  // used by alternate hops
     DevBuf sizes;
     HostPinned sizes_host;  // [0] publication sequence, [1..3L] per-hop sizes, [3L+1] bad seed
