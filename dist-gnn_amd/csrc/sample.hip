@@ -1094,8 +1094,57 @@ __global__ __launch_bounds__(kTileRows, DGS_BIAS_HUB_WAVES) void k_bias_hub(Bias
   flush(h);
 }
 
-// One workgroup per hub row: its 8 half-waves reduce interleaved subsets of the row's worker
-// slots, then half-wave 0 merges the 8 partial lists and emits the picks.
+#ifndef DGS_MERGE_HALF_SLOTS
+#define DGS_MERGE_HALF_SLOTS 8
+#endif
+// Rows whose chunks went to at most this many workers are merged by one half-wave each (8 rows
+// per workgroup at once, no barrier); the others by a whole workgroup.
+constexpr int64_t kMergeHalfSlots = DGS_MERGE_HALF_SLOTS;
+
+// The worker slots of row h from w0 on (every `step`-th pair when per == 2) pushed into `top`.
+__device__ __forceinline__ void merge_slots(const BiasHubArgs &a, HalfTopK &top, int64_t h,
+                                            int64_t wf, int64_t wl, int64_t first, int64_t step,
+                                            int64_t total, int64_t nw, int64_t k, int l) {
+  // k <= 16: two workers' lists per batch (lanes 0-15 and 16-31), else one
+  const int per = k <= 16 ? 2 : 1;
+  const int part = per == 2 ? (l >> 4) : 0;
+  const int e = per == 2 ? (l & 15) : l;
+  // a worker's list is sorted (descending); the second list of a pair is read in reverse
+  // so the 32 lanes hold a bitonic sequence
+  const int er = part ? 15 - e : e;
+  for (int64_t w0 = wf + (int64_t)per * first; w0 <= wl; w0 += step * per) {
+    const int64_t w = w0 + part;
+    bool have = w <= wl && bias_worker_c0(total, w, nw) != bias_worker_c0(total, w + 1, nw);
+    const int64_t slot = w + h;
+    const int n = have ? a.ccnt[slot] : 0;
+    const bool valid = er < n;
+    float key_i = -__builtin_inff();
+    int32_t i = INT32_MAX;
+    if (valid) {
+      key_i = a.ckey[slot * k + er];
+      i = a.cidx[slot * k + er];
+    }
+    top.push_bitonic(key_i, i, valid, k, l, per == 1);
+  }
+}
+
+// Writes row h's k picks (lane l < k: the l-th best, index idx_l).
+__device__ __forceinline__ void merge_emit(const BiasHubArgs &a, int64_t S, int64_t h, int32_t idx_l,
+                                           int64_t k, int l) {
+  const int64_t r = a.hub.row[h];
+  const RowInfo ri = a.rowinfo[r];
+  const int64_t out = a.boff[r / kTileRows] + a.tpre[r];
+  if (l < k) {
+    const int64_t v = as_global(ri.ptr)[idx_l];
+    a.rowpos[out + l] = r;
+    a.col[out + l] = v;
+    table_record(a.table, v, S + out + l);
+  }
+}
+
+// Reduces each hub row's worker slots to its k picks.  Rows with few slots: one half-wave per
+// row.  The others: one workgroup per row, whose 8 half-waves reduce interleaved subsets of the
+// slots before half-wave 0 merges the 8 partial lists and emits the picks.
 __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
   latency_prio();
   __shared__ float s_key[8][32];
@@ -1107,30 +1156,18 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
   const int64_t nw = bias_workers(total, a.nworkers);
   const int64_t k = a.k;
   const int l = threadIdx.x & 31, g = threadIdx.x >> 5;
+  for (int64_t h = (int64_t)blockIdx.x * 8 + g; h < H; h += (int64_t)gridDim.x * 8) {
+    const int64_t wf = a.wfirst[h], wl = a.wlast[h];
+    if (wl - wf + 1 > kMergeHalfSlots) continue;
+    HalfTopK top;
+    merge_slots(a, top, h, wf, wl, 0, 1, total, nw, k, l);
+    merge_emit(a, S, h, l < k && top.bi != INT32_MAX ? top.bi : INT32_MAX, k, l);
+  }
   for (int64_t h = blockIdx.x; h < H; h += gridDim.x) {
     const int64_t wf = a.wfirst[h], wl = a.wlast[h];
+    if (wl - wf + 1 <= kMergeHalfSlots) continue;
     HalfTopK top;
-    // k <= 16: two workers' lists per batch (lanes 0-15 and 16-31), else one
-    const int per = k <= 16 ? 2 : 1;
-    const int part = per == 2 ? (l >> 4) : 0;
-    const int e = per == 2 ? (l & 15) : l;
-    // a worker's list is sorted (descending); the second list of a pair is read in reverse
-    // so the 32 lanes hold a bitonic sequence
-    const int er = part ? 15 - e : e;
-    for (int64_t w0 = wf + (int64_t)per * g; w0 <= wl; w0 += 8 * per) {
-      const int64_t w = w0 + part;
-      bool have = w <= wl && bias_worker_c0(total, w, nw) != bias_worker_c0(total, w + 1, nw);
-      const int64_t slot = w + h;
-      const int n = have ? a.ccnt[slot] : 0;
-      const bool valid = er < n;
-      float key_i = -__builtin_inff();
-      int32_t i = INT32_MAX;
-      if (valid) {
-        key_i = a.ckey[slot * k + er];
-        i = a.cidx[slot * k + er];
-      }
-      top.push_bitonic(key_i, i, valid, k, l, per == 1);
-    }
+    merge_slots(a, top, h, wf, wl, g, 8, total, nw, k, l);
     // the 8 half-waves' lists (sorted, only the first k count: an entry past its own list's
     // k-th can not be among the k best of the union) merged pairwise in a tree
     const bool mine = l < k && top.bi != INT32_MAX;
@@ -1156,17 +1193,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
       }
       __syncthreads();
     }
-    if (g == 0) {
-      const int64_t r = a.hub.row[h];
-      const RowInfo ri = a.rowinfo[r];
-      const int64_t out = a.boff[r / kTileRows] + a.tpre[r];
-      if (l < k) {
-        const int64_t v = as_global(ri.ptr)[s_idx[0][l]];
-        a.rowpos[out + l] = r;
-        a.col[out + l] = v;
-        table_record(a.table, v, S + out + l);
-      }
-    }
+    if (g == 0) merge_emit(a, S, h, s_idx[0][l], k, l);
     __syncthreads();
   }
 }
