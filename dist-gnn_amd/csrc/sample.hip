@@ -34,7 +34,8 @@ constexpr int kBiasHubT = 1024;  // biased rows above this degree are split acro
 #define DGS_BIAS_CHUNK 256
 #endif
 constexpr int kBiasChunk = DGS_BIAS_CHUNK;  // edges per biased hub chunk (32 lanes x 8 draws)
-constexpr int kBiasHubBlocks = 1024;  // workgroups of the biased hub kernel (8 half-waves each)
+constexpr int kBiasHubBlocks = 768;  // workgroups of the biased hub kernel (8 half-waves each): 3 of
+                                      // its 4 resident waves per SIMD, room for the other batches
 constexpr int kHubBlocks = 1536; // workgroups of the hub kernel: 6 of 8 waves per SIMD, so the
                                  // other batches in flight (feature gather) find free slots
 constexpr int kMaxPicksLds = 512;
@@ -46,6 +47,16 @@ int hub_blocks() {
     const char *e = getenv("DGS_HUB_BLOCKS");
     const int v = e ? atoi(e) : 0;
     return v > 0 ? v : kHubBlocks;
+  }();
+  return n;
+}
+
+// Workgroups of the biased hub kernel; DGS_BIAS_HUB_BLOCKS overrides (occupancy experiments).
+int bias_hub_blocks() {
+  static const int n = [] {
+    const char *e = getenv("DGS_BIAS_HUB_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : kBiasHubBlocks;
   }();
   return n;
 }
@@ -1278,7 +1289,7 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     DGS_CHECK(k <= 32, "biased sampling supports num_picks <= 32 (rowwise_sampling_bias.cu:73)");
     float *cdf = nullptr;
     const dim3 grid((unsigned)ceil_div(S, kBiasRowsPerBlock));
-    const int64_t nworkers = (int64_t)kBiasHubBlocks * (kTileRows / 32);
+    const int64_t nworkers = (int64_t)bias_hub_blocks() * (kTileRows / 32);
     BiasHubArgs ba{};
     if (bias_hubs) {
       const int64_t slots = nworkers + S;
@@ -1290,7 +1301,7 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
       int32_t *wfirst = ccnt + slots;
       ba = BiasHubArgs{src, Sc, k, launch_seed, rowinfo, tpre, boff, hub, ckey, cidx, ccnt,
                        wfirst, wfirst + S, nworkers, rowpos, col, table};
-      hipLaunchKernelGGL(k_bias_hub, dim3(kBiasHubBlocks), dim3(kTileRows), 0, st, ba);
+      hipLaunchKernelGGL(k_bias_hub, dim3(bias_hub_blocks()), dim3(kTileRows), 0, st, ba);
       DGS_LAUNCH_CHECK();
     }
     if (replace) {
