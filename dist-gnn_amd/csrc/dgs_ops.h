@@ -78,7 +78,7 @@ struct RowSrc {
 
 struct HopScratch {
   DevBuf rowinfo, tpre, bsum, boff, hub, hubcount, hubslot, rowpos, slot_of, tkey, tval, tlab,
-      misc, cdf, cand;
+      misc, cdf, cand, flags;
   HostPinned host;
   uint64_t table_cap = 0;  // capacity currently allocated and clean
   uint64_t hop_serial = 0;  // parity selects the hub counter of a hop

@@ -151,9 +151,11 @@ __device__ __forceinline__ int64_t first_flags(const int64_t *a, int64_t na, con
   return cnt;
 }
 
+// Pass 1 also leaves each thread's flags (one byte, bit j = element i0 + j) for pass 2, which
+// then needs no second round of random table reads.
 __global__ __launch_bounds__(kThreads) void k_dcount(const int64_t *a, Count nac,
                                                      const int64_t *b, const int64_t *d_nb,
-                                                     Table t, int64_t *tcnt) {
+                                                     Table t, int64_t *tcnt, uint8_t *flags) {
   latency_prio();
   __shared__ int64_t lds[kThreads / 64];
   const int64_t na = nac.get();
@@ -163,6 +165,10 @@ __global__ __launch_bounds__(kThreads) void k_dcount(const int64_t *a, Count nac
   int64_t x[kCompactItems];
   bool f[kCompactItems];
   const int64_t cnt = first_flags(a, na, b, n, t, i0, x, f);
+  uint32_t fb = 0;
+#pragma unroll
+  for (int j = 0; j < kCompactItems; ++j) fb |= (uint32_t)f[j] << j;
+  flags[(int64_t)blockIdx.x * kThreads + threadIdx.x] = (uint8_t)fb;
   const int64_t s = block_sum<kThreads>(cnt, lds);
   if (threadIdx.x == 0) tcnt[blockIdx.x] = s;
 }
@@ -170,8 +176,8 @@ __global__ __launch_bounds__(kThreads) void k_dcount(const int64_t *a, Count nac
 __global__ __launch_bounds__(kThreads) void k_dscatter(const int64_t *a, Count nac,
                                                        const int64_t *b, const int64_t *d_nb,
                                                        Table t, const int64_t *tcnt,
-                                                       int64_t *unique, int64_t *d_nunique,
-                                                       HostSizes pub) {
+                                                       const uint8_t *flags, int64_t *unique,
+                                                       int64_t *d_nunique, HostSizes pub) {
   latency_prio();
   __shared__ int64_t lds[kThreads / 64];
   const int64_t na = nac.get();
@@ -183,9 +189,16 @@ __global__ __launch_bounds__(kThreads) void k_dscatter(const int64_t *a, Count n
   int64_t pre = 0;
   for (int64_t j = threadIdx.x; j < tile; j += kThreads) pre += tcnt[j];
   const int64_t i0 = tile * kCompactTile + (int64_t)threadIdx.x * kCompactItems;
+  const uint32_t fb = flags[tile * kThreads + threadIdx.x];
   int64_t x[kCompactItems];
   bool f[kCompactItems];
-  const int64_t cnt = first_flags(a, na, b, n, t, i0, x, f);
+#pragma unroll
+  for (int j = 0; j < kCompactItems; ++j) {
+    const int64_t i = i0 + j < n ? i0 + j : n - 1;
+    x[j] = i < na ? a[i] : b[i - na];
+    f[j] = (fb >> j) & 1u;
+  }
+  const int64_t cnt = __builtin_popcount(fb);
   const int64_t base = block_sum<kThreads>(pre, lds);
   int64_t tot;
   int64_t ex = base + block_exclusive_scan<kThreads>(cnt, &tot, lds);
@@ -294,11 +307,14 @@ void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64
   if (t.direct) {
     const int64_t ntiles = ceil_div(n_ub > 0 ? n_ub : 1, kCompactTile);
     int64_t *tcnt = bcnt;  // ws.misc holds >= nblk >= ntiles words
+    ws.flags.ensure((size_t)(ntiles * kThreads));
+    uint8_t *flags = ws.flags.as<uint8_t>();
     hipLaunchKernelGGL(k_dcount, dim3((unsigned)ntiles), dim3(kThreads), 0, st, seeds, Sc, col,
-                       d_nnz, t, tcnt);
+                       d_nnz, t, tcnt, flags);
     DGS_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_dscatter, dim3((unsigned)ntiles), dim3(kThreads), 0, st, seeds, Sc,
-                       col, d_nnz, t, (const int64_t *)tcnt, unique, d_nunique, pub);
+                       col, d_nnz, t, (const int64_t *)tcnt, (const uint8_t *)flags, unique,
+                       d_nunique, pub);
     DGS_LAUNCH_CHECK();
     const RelabelTail tail{seeds, Sc, d_nnz, t, (int)!seeds_unique, out_row, out_col, nblk};
     if (defer) {
