@@ -29,8 +29,9 @@ struct Table {
 
 // The last pass of a hop's relabel (direct layout): out_col[e] = lab[col[e]] in place,
 // out_row[e] = lab[seeds[r]] when the seeds may repeat (else label(r) == r), then every touched
-// node's val returns to empty.  Kept as a descriptor so the sampler can run it in the same
-// launch as the next hop's prep (which uses the other table).
+// node's val returns to empty.  The touched nodes are exactly the hop's unique ids, so the reset
+// is one store per unique node (not one per seed and sampled edge).  Kept as a descriptor so the
+// sampler can run it in the same launch as the next hop's prep (which uses the other table).
 struct RelabelTail {
   const int64_t *seeds;
   Count Sc;
@@ -39,7 +40,9 @@ struct RelabelTail {
   int remap_rows;
   int64_t *out_row;
   int64_t *out_col;
-  int64_t nblk;  // 256-thread blocks covering max(S, nnz) (upper bounds)
+  const int64_t *unique;    // the hop's unique ids (first-occurrence order)
+  const int64_t *d_nuniq;   // their count (device)
+  int64_t nblk;  // 256-thread blocks covering S + nnz (upper bounds; >= nnz and >= U)
 };
 
 #ifdef __HIPCC__
@@ -48,19 +51,16 @@ __device__ __forceinline__ int32_t *dval(const Table &t, int64_t x) { return t.v
 __device__ __forceinline__ int32_t *dlab(const Table &t, int64_t x) { return t.val + 2 * x + 1; }
 
 __device__ __forceinline__ void relabel_tail_block(const RelabelTail &r, int64_t blk) {
-  const int64_t na = r.Sc.get();
   const int64_t nb = *r.d_nb;
+  const int64_t nu = *r.d_nuniq;
   const int64_t e = blk * 256 + threadIdx.x;
   if (e < nb) {
     const int64_t v = r.out_col[e];
     r.out_col[e] = *dlab(r.t, v);
     if (r.remap_rows) r.out_row[e] = *dlab(r.t, r.seeds[r.out_row[e]]);
-    *dval(r.t, v) = kTableNoPos;
   }
-  if (e < na) {
-    const int64_t s = r.seeds[e];
-    if ((uint64_t)s < (uint64_t)r.t.n) *dval(r.t, s) = kTableNoPos;
-  }
+  // (the label loads above read the other word of the pair: no conflict with the resets)
+  if (e < nu) *dval(r.t, r.unique[e]) = kTableNoPos;
 }
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {

@@ -316,7 +316,8 @@ void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64
                        col, d_nnz, t, (const int64_t *)tcnt, (const uint8_t *)flags, unique,
                        d_nunique, pub);
     DGS_LAUNCH_CHECK();
-    const RelabelTail tail{seeds, Sc, d_nnz, t, (int)!seeds_unique, out_row, out_col, nblk};
+    const RelabelTail tail{seeds, Sc, d_nnz, t, (int)!seeds_unique, out_row, out_col,
+                           unique, d_nunique, nblk};
     if (defer) {
       *defer = tail;  // the caller launches it with the next hop's prep
     } else {
