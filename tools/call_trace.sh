@@ -12,5 +12,5 @@ for v in uniform bias; do
   [ $v = bias ] && extra="--bias"
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/$v -- \
     python3 bench.py --depth 1 --steps 100 --warmup 10 --no-cpu-baseline $extra > $O/$v.log 2>&1
-  python3 tools/call_breakdown.py "$(find $O/$v -name '*kernel_trace.csv' | head -1)" > $O/$v.txt
+  python3 tools/call_breakdown.py "$(ls -t $(find $O/$v -name '*kernel_trace.csv') | head -n 1)" > $O/$v.txt
 done
