@@ -1003,10 +1003,15 @@ __global__ __launch_bounds__(kTileRows, DGS_BIAS_HUB_WAVES) void k_bias_hub(Bias
     const int64_t i0 = q * kBiasChunk + l;
     const bool whole = q * kBiasChunk + kBiasChunk <= deg;  // no edge of the chunk past the row
     float p[kT];
+    {
+      // row-local edge indices fit 32 bits (deg < 2^31): 32-bit offset arithmetic, one
+      // 64-bit address add per load (the 64-bit form took 14 more VGPRs)
+      const uint32_t i32 = (uint32_t)i0, last = (uint32_t)(deg - 1);
 #pragma unroll
-    for (int t = 0; t < kT; ++t) {
-      const int64_t i = i0 + 32 * t;
-      p[t] = pr[whole || i < deg ? i : deg - 1];
+      for (int t = 0; t < kT; ++t) {
+        const uint32_t i = i32 + 32u * t;
+        p[t] = pr[whole ? i : (i < last ? i : last)];
+      }
     }
     // this lane's kT draws j = jb + kT q + t lie in kT / 4 + 1 consecutive Philox blocks
     // (uniform control flow -- lanes' chain offsets differ, a lazy per-lane refill would diverge
@@ -1044,6 +1049,11 @@ __global__ __launch_bounds__(kTileRows, DGS_BIAS_HUB_WAVES) void k_bias_hub(Bias
     uint32_t w2[kT + 1];
 #pragma unroll
     for (int e = 0; e < kT + 1; ++e) w2[e] = bitsel(m2, wv[e + 2], wv[e]);
+    // every draw of the chunk is computed before the first probability is used, so the
+    // probability loads' latency hides under all of the chunk's Philox work (the scheduler
+    // otherwise starts the filter after a third of it; with the 32-bit indices: +3.8 %)
+#pragma unroll
+    for (int e = 0; e < kT + 1; ++e) asm volatile("" ::"v"(w2[e]));
     // The chunk's filter threshold, fixed for its 16 steps: this worker's k-th key once its list
     // is full, or the best k-th any worker of the row has published -- both lower bounds of the
     // row's final k-th key, so an edge the cheap test rejects can not be among the row's picks.
