@@ -231,6 +231,17 @@ def main():
     torch.cuda.synchronize()
     iso = dgs.ops.profile_read()
     dgs.ops.profile_enable(False)
+    # SURVEY 8(d) metric (2) as defined there: algorithmic bytes / wall time of one synchronous
+    # _CAPI_get_feature call (host launch + kernel + synchronisation), median over the side pass
+    call_ms = []
+    for n in side_nids:
+        tc = time.perf_counter()
+        server._CAPI_get_feature(n)
+        torch.cuda.synchronize()
+        call_ms.append((time.perf_counter() - tc) * 1e3)
+    call_i = int(np.argsort(call_ms)[len(call_ms) // 2])
+    call_gbps = (side_nids[call_i].numel() * (2 * args.dim * 4 + 8) / (call_ms[call_i] * 1e-3) / 1e9
+                 if call_ms else 0.0)
 
     row_bytes = args.dim * 4
     gather_bytes = rows * (2 * row_bytes + 8)  # read row + write row + read nid
@@ -292,6 +303,7 @@ def main():
                                   if prof["gather_ms"] > 0 else 0.0),
         "gather_GBps": achieved,
         "gather_GBps_wall": gbytes_all / elapsed / 1e9,
+        "gather_GBps_sync_call": call_gbps,
         "sampled_edges_per_step": edges_all / args.steps,
         "gathered_rows_per_step": rows_all / args.steps,
         "gather_kernel_ms_per_step": prof["gather_ms"] / args.steps,
