@@ -920,7 +920,20 @@ __device__ __forceinline__ int64_t bias_workers(int64_t total, int64_t max_worke
 #ifndef DGS_BIAS_HUB_WAVES
 #define DGS_BIAS_HUB_WAVES 1
 #endif
-__global__ __launch_bounds__(kTileRows, DGS_BIAS_HUB_WAVES) void k_bias_hub(BiasHubArgs a) {
+__global__ __launch_bounds__(kTileRows, DGS_BIAS_HUB_WAVES) void k_bias_hub(BiasHubArgs a,
+                                                                           const int64_t *bsum,
+                                                                           int64_t *boff,
+                                                                           int64_t *d_nnz) {
+  if (blockIdx.x == 0) {
+    // the hop's tile-offset scan (k_scan_hop's job), which k_sample_bias after it reads
+    __shared__ int64_t lds[kTileRows / 64];
+    const int64_t nb = (a.Sc.get() + kTileRows - 1) / kTileRows;
+    const int64_t tot = block_scan_range<kTileRows, 8>(bsum, nb, boff, lds);
+    if (threadIdx.x == 0) {
+      boff[nb] = tot;
+      *d_nnz = tot;
+    }
+  }
   const int64_t S = a.Sc.get();
   const int64_t G = (S + 15) / 16;
   const uint64_t packed = (uint64_t)*a.hub.count;
@@ -1281,7 +1294,8 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     DGS_HIP(hipMemsetAsync(d_nnz, 0, sizeof(int64_t), st));
     return;
   }
-  if (!use_hubs) {
+  // (the hub kernels' workgroup 0 does this scan when they run: one launch fewer per hop)
+  if (!use_hubs && !bias_hubs) {
     hipLaunchKernelGGL(k_scan_hop, dim3(1), dim3(kScanThreads), 0, st, bsum,
                        bias_replace ? (const int64_t *)tsum : nullptr, Sc, boff, tboff, d_nnz,
                        bsum + 2 * nb + 1);
@@ -1322,7 +1336,8 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
       int32_t *wfirst = ccnt + slots;
       ba = BiasHubArgs{src, Sc, k, launch_seed, rowinfo, tpre, boff, hub, ckey, cidx, ccnt,
                        wfirst, wfirst + S, nworkers, rowpos, col, table};
-      hipLaunchKernelGGL(k_bias_hub, dim3(bias_hub_blocks()), dim3(kTileRows), 0, st, ba);
+      hipLaunchKernelGGL(k_bias_hub, dim3(bias_hub_blocks()), dim3(kTileRows), 0, st, ba,
+                         (const int64_t *)bsum, boff, d_nnz);
       DGS_LAUNCH_CHECK();
     }
     if (replace) {
