@@ -694,18 +694,17 @@ struct HalfTopK {
 };
 
 template <bool kReplace>
-__global__ __launch_bounds__(kTileRows) void k_sample_bias(
-    RowSrc src, Count Sc, int64_t k, uint64_t seed, const RowInfo *__restrict__ rowinfo,
+__device__ __forceinline__ void sample_bias_block(
+    const RowSrc &src, Count Sc, int64_t k, uint64_t seed, const RowInfo *__restrict__ rowinfo,
     const int32_t *__restrict__ tpre, const int64_t *__restrict__ boff,
     const int32_t *__restrict__ tpre2, const int64_t *__restrict__ tboff, float *cdf,
-    int64_t *__restrict__ rowpos, int64_t *__restrict__ col, Table table,
-    const int64_t *__restrict__ hubid) {
-  latency_prio();
+    int64_t *__restrict__ rowpos, int64_t *__restrict__ col, const Table &table,
+    const int64_t *__restrict__ hubid, int64_t blk) {
   const int64_t S = Sc.get();
   const int64_t G = (S + 15) / 16;  // reference grid: ceil(S / TILE_SIZE=16)
   const int hw = threadIdx.x >> 5, l = threadIdx.x & 31;
   {
-    const int64_t r = (int64_t)blockIdx.x * kBiasRowsPerBlock + hw;
+    const int64_t r = blk * kBiasRowsPerBlock + hw;
     if (r >= S) return;
     const RowInfo ri = rowinfo[r];
     const int64_t deg = ri_deg(ri);
@@ -864,6 +863,18 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
       }
     }
   }
+}
+
+template <bool kReplace>
+__global__ __launch_bounds__(kTileRows) void k_sample_bias(
+    RowSrc src, Count Sc, int64_t k, uint64_t seed, const RowInfo *__restrict__ rowinfo,
+    const int32_t *__restrict__ tpre, const int64_t *__restrict__ boff,
+    const int32_t *__restrict__ tpre2, const int64_t *__restrict__ tboff, float *cdf,
+    int64_t *__restrict__ rowpos, int64_t *__restrict__ col, Table table,
+    const int64_t *__restrict__ hubid) {
+  latency_prio();
+  sample_bias_block<kReplace>(src, Sc, k, seed, rowinfo, tpre, boff, tpre2, tboff, cdf, rowpos,
+                              col, table, hubid, blockIdx.x);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1190,8 +1201,7 @@ __device__ __forceinline__ void merge_emit(const BiasHubArgs &a, int64_t S, int6
 // Reduces each hub row's worker slots to its k picks.  Rows with few slots: one half-wave per
 // row.  The others: one workgroup per row, whose 8 half-waves reduce interleaved subsets of the
 // slots before half-wave 0 merges the 8 partial lists and emits the picks.
-__global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
-  latency_prio();
+__device__ __forceinline__ void bias_merge_block(const BiasHubArgs &a, int64_t blk, int64_t nblk) {
   __shared__ float s_key[8][32];
   __shared__ int32_t s_idx[8][32];
   const int64_t S = a.Sc.get();
@@ -1201,14 +1211,14 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
   const int64_t nw = bias_workers(total, a.nworkers);
   const int64_t k = a.k;
   const int l = threadIdx.x & 31, g = threadIdx.x >> 5;
-  for (int64_t h = (int64_t)blockIdx.x * 8 + g; h < H; h += (int64_t)gridDim.x * 8) {
+  for (int64_t h = blk * 8 + g; h < H; h += nblk * 8) {
     const int64_t wf = a.wfirst[h], wl = a.wlast[h];
     if (wl - wf + 1 > kMergeHalfSlots) continue;
     HalfTopK top;
     merge_slots(a, top, h, wf, wl, 0, 1, total, nw, k, l);
     merge_emit(a, S, h, l < k && top.bi != INT32_MAX ? top.bi : INT32_MAX, k, l);
   }
-  for (int64_t h = blockIdx.x; h < H; h += gridDim.x) {
+  for (int64_t h = blk; h < H; h += nblk) {
     const int64_t wf = a.wfirst[h], wl = a.wlast[h];
     if (wl - wf + 1 <= kMergeHalfSlots) continue;
     HalfTopK top;
@@ -1241,6 +1251,24 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
     if (g == 0) merge_emit(a, S, h, s_idx[0][l], k, l);
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
+  latency_prio();
+  bias_merge_block(a, blockIdx.x, gridDim.x);
+}
+
+// The biased hop's non-hub rows (workgroups [0, row_blocks)) and its hub-row merge (the rest) in
+// one launch: both only need the hub kernel before them (one launch fewer per hop).
+__global__ __launch_bounds__(kTileRows) void k_bias_rows_merge(
+    BiasHubArgs a, const int32_t *__restrict__ tpre2, const int64_t *__restrict__ tboff,
+    int64_t row_blocks, int64_t merge_blocks) {
+  latency_prio();
+  if ((int64_t)blockIdx.x < row_blocks)
+    sample_bias_block<false>(a.src, a.Sc, a.k, a.seed, a.rowinfo, a.tpre, a.boff, tpre2, tboff,
+                             nullptr, a.rowpos, a.col, a.table, a.hub.hubid, blockIdx.x);
+  else
+    bias_merge_block(a, (int64_t)blockIdx.x - row_blocks, merge_blocks);
 }
 
 }  // namespace
@@ -1351,9 +1379,17 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
                          launch_seed, rowinfo, tpre, boff, tpre2, tboff, cdf, rowpos, col, table,
                          (const int64_t *)nullptr);
     } else {
+      if (bias_hubs) {
+        const int64_t mb = std::min<int64_t>(S, 2048);
+        hipLaunchKernelGGL(k_bias_rows_merge, dim3((unsigned)(grid.x + mb)), dim3(kTileRows), 0,
+                           st, ba, (const int32_t *)tpre2, (const int64_t *)tboff,
+                           (int64_t)grid.x, mb);
+        DGS_LAUNCH_CHECK();
+        return;
+      }
       hipLaunchKernelGGL(k_sample_bias<false>, grid, dim3(kTileRows), 0, st, src, Sc, k,
                          launch_seed, rowinfo, tpre, boff, tpre2, tboff, cdf, rowpos, col, table,
-                         bias_hubs ? (const int64_t *)hub.hubid : nullptr);
+                         (const int64_t *)nullptr);
     }
     DGS_LAUNCH_CHECK();
     if (bias_hubs) {
