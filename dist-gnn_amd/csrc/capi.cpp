@@ -74,6 +74,19 @@ std::unique_lock<std::mutex> op_scratch(hipStream_t st, HopScratch **ws) {
   *ws = &o->ws;
   return std::unique_lock<std::mutex>(o->mu);
 }
+// `consumer` waits (on the device) for the work enqueued on `producer` so far.  One event per
+// calling thread and device: a wait already enqueued keeps the record it saw, so the event can
+// be recorded again at once.
+void stream_wait_impl(void *producer, void *consumer) {
+  thread_local std::vector<hipEvent_t> evs;
+  int dev = 0;
+  DGS_HIP(hipGetDevice(&dev));
+  if ((int)evs.size() <= dev) evs.resize((size_t)dev + 1, nullptr);
+  if (!evs[dev]) DGS_HIP(hipEventCreateWithFlags(&evs[dev], hipEventDisableTiming));
+  hipEvent_t ev = evs[dev];
+  DGS_HIP(hipEventRecord(ev, S(producer)));
+  DGS_HIP(hipStreamWaitEvent(S(consumer), ev, 0));
+}
 }  // namespace
 
 struct dgs_p2p_server {
@@ -180,17 +193,18 @@ int dgs_index_select_device(const void *data, int64_t row_bytes, const void *nid
 }
 
 int dgs_stream_wait(void *producer, void *consumer) {
+  return guard([&] { stream_wait_impl(producer, consumer); });
+}
+
+int dgs_loader_gather(dgs_feature_server *fs, void *producer, void *consumer,
+                      const int64_t *nids, int64_t n, void *feat_out, const void *labels,
+                      int64_t label_row_bytes, const int64_t *seeds, int64_t n_seeds,
+                      void *label_out) {
   return guard([&] {
-    // one event per calling thread and device: a wait already enqueued keeps the record it
-    // saw, so the event can be recorded again at once
-    thread_local std::vector<hipEvent_t> evs;
-    int dev = 0;
-    DGS_HIP(hipGetDevice(&dev));
-    if ((int)evs.size() <= dev) evs.resize((size_t)dev + 1, nullptr);
-    if (!evs[dev]) DGS_HIP(hipEventCreateWithFlags(&evs[dev], hipEventDisableTiming));
-    hipEvent_t ev = evs[dev];
-    DGS_HIP(hipEventRecord(ev, S(producer)));
-    DGS_HIP(hipStreamWaitEvent(S(consumer), ev, 0));
+    stream_wait_impl(producer, consumer);
+    if (fs && n > 0) fs->s->gather(nids, n, feat_out, S(consumer));
+    if (labels && n_seeds > 0)
+      gather_plain(labels, label_row_bytes, seeds, 8, n_seeds, label_out, S(consumer));
   });
 }
 
@@ -378,6 +392,19 @@ int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_see
     DGS_CHECK((flags & ~DGS_SAMPLE_HOST_ASYNC) == 0, "sample_begin: unknown flags");
     s->s->sample_begin(dev_ptr(seeds, "seeds"), n_seeds, fan_out, L, replace != 0, frontiers,
                        rows, cols, S(stream), launch_seeds, (flags & DGS_SAMPLE_HOST_ASYNC) != 0);
+  });
+}
+
+int dgs_sampler_sample_begin_after(dgs_sampler *s, void *wait_for, const int64_t *seeds,
+                                   int64_t n_seeds, const int64_t *fan_out, int L, int replace,
+                                   int64_t *const *frontiers, int64_t *const *rows,
+                                   int64_t *const *cols, const uint64_t *launch_seeds, int flags,
+                                   void *stream) {
+  return guard([&] {
+    DGS_CHECK((flags & ~DGS_SAMPLE_HOST_ASYNC) == 0, "sample_begin: unknown flags");
+    if (wait_for) stream_wait_impl(wait_for, stream);
+    s->s->sample_begin(seeds, n_seeds, fan_out, L, replace != 0, frontiers, rows, cols,
+                       S(stream), launch_seeds, (flags & DGS_SAMPLE_HOST_ASYNC) != 0);
   });
 }
 

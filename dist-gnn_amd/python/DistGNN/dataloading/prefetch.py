@@ -73,6 +73,11 @@ class PrefetchLoader:
             # the per-batch label gather reads device memory (host labels are copied once)
             labels = labels.to(self.device).contiguous()
         self.sampler, self.server, self.labels = sampler, server, labels
+        self._label_row_bytes = 0
+        if labels is not None:
+            self._label_row_bytes = labels.element_size()
+            for d in labels.shape[1:]:
+                self._label_row_bytes *= int(d)
         self.fan_out, self.replace = list(fan_out), bool(replace)
         self._seeds = iter(seeds_iter)
         self._exhausted = False
@@ -104,11 +109,11 @@ class PrefetchLoader:
         # the caller may drop its seeds at once: their memory must outlive B's reads
         seeds.record_stream(self._streams[w])
         prep = self.sampler._prepare(seeds, self.fan_out)  # int64 seeds + outputs, on C
-        dgs.ops._stream_wait(cur, st)
+        # B waits for C (after the allocations), then the call is enqueued: one C-ABI call.
         # B is not touched again before result(): the sampler's launcher thread may issue
         # the launches.  The sampler draws the launch seeds once it has accepted the call.
         pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, _HOST_ASYNC,
-                                               st)
+                                               st, wait_for=cur)
         self._inflight.append((pending, prep[0], w))
 
     def __iter__(self):
@@ -130,22 +135,20 @@ class PrefetchLoader:
             self.close()
             raise
         # C after B (the sample call); the feature and label gathers then run on C, whose
-        # hardware queue the batch streams do not use
-        dgs.ops._stream_wait(st, cur)
-        x = None
+        # hardware queue the batch streams do not use -- the wait and both gathers in one
+        # C-ABI call.  (The label gather depends on the seeds only; on C it stays off the
+        # batch's critical path: issued on B in front of the sample call, it delayed hop 0
+        # while it waited for a slot on CUs the other batches fill.)
+        x = y = None
+        front = None
         if self.server is not None:
             front = blocks[-1][1]
             x = self.server._get_feature_alloc(front)
-            self.server._get_feature_into(front, x, cur)
-        y = None
         if self.labels is not None:
-            # the label gather depends on the seeds only; on C it stays off the batch's
-            # critical path (issued on B in front of the sample call, it delayed hop 0 while
-            # it waited for a slot on CUs the other batches fill: a 20-step run's first batch
-            # came 0.17 ms later, 2.43-2.50 -> 2.59-2.68 G edges/s over 5 same-box runs)
             y = torch.empty((s64.numel(),) + tuple(self.labels.shape[1:]),
                             dtype=self.labels.dtype, device=self.device)
-            dgs.ops._index_select_into(self.labels, s64, y, cur)
+        dgs.ops._loader_gather(self.server, st, cur, front, x, self.labels,
+                               self._label_row_bytes, s64, y)
         dt = self.sampler._id_dtype
         if dt != torch.int64:  # int32 graphs: cast on the caller's stream, now ordered after B
             cast, cur_seeds = [], blocks[0][0]

@@ -117,19 +117,27 @@ class P2PCacheSampler:
         return self._begin_prepared(seeds, prep, replace, launch_seeds, host_async,
                                     stream_ptr(prep[0].device))
 
-    def _begin_prepared(self, seeds, prep, replace, launch_seeds, host_async, stream):
+    def _begin_prepared(self, seeds, prep, replace, launch_seeds, host_async, stream,
+                        wait_for=None):
         """Enqueues a call whose int64 seeds and output buffer _prepare made, on `stream`
         (a c_void_p or int HIP stream).  PrefetchLoader allocates on the caller's stream and
-        orders the batch stream after those allocations before it launches."""
+        orders the batch stream after those allocations before it launches: `wait_for` (an int
+        HIP stream) makes `stream` wait for it first, in the same C-ABI call."""
         s, L, fo, caps, total, buf, ptrs = prep
         st = stream if isinstance(stream, c_vp) else c_vp(stream)
         ls = None
         if L and launch_seeds is not None:
             ls = (ctypes.c_uint64 * L)(*[int(x) & 0xFFFFFFFFFFFFFFFF for x in launch_seeds])
-        if L:
+        if L and wait_for is not None:
+            check(lib.dgs_sampler_sample_begin_after(self._h, c_vp(wait_for), c_vp(s.data_ptr()),
+                                                     s.numel(), fo, L, int(bool(replace)), *ptrs,
+                                                     ls, 1 if host_async else 0, st))
+        elif L:
             check(lib.dgs_sampler_sample_begin(self._h, c_vp(s.data_ptr()), s.numel(), fo, L,
                                                int(bool(replace)), *ptrs, ls,
                                                1 if host_async else 0, st))
+        elif wait_for is not None:
+            check(lib.dgs_stream_wait(c_vp(wait_for), st))
         return _PendingSample(self, seeds, s, L, caps, total, buf, st)
 
     def _sample(self, seeds, fan_out, replace, launch_seeds):

@@ -235,6 +235,20 @@ def _index_select_into(data, nid, out, stream):
                                       ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))
 
 
+def _loader_gather(server, producer, consumer, nids, x, labels, label_row_bytes, seeds, y):
+    """ADDITIVE (PrefetchLoader): `consumer` waits for `producer`, then x = features[nids]
+    (server may be None) and y = labels[seeds] (labels may be None), on `consumer`; one C-ABI
+    call.  All tensors contiguous device tensors, nids and seeds int64."""
+    vp = ctypes.c_void_p
+    check(lib.dgs_loader_gather(
+        server._h if server is not None else None, vp(producer), vp(consumer),
+        vp(nids.data_ptr()) if nids is not None else None,
+        nids.numel() if nids is not None else 0, vp(x.data_ptr()) if x is not None else None,
+        vp(labels.data_ptr()) if labels is not None else None, int(label_row_bytes),
+        vp(seeds.data_ptr()), seeds.numel() if labels is not None else 0,
+        vp(y.data_ptr()) if y is not None else None))
+
+
 def _stream_wait(producer, consumer):
     """ADDITIVE: HIP stream `consumer` waits for the work enqueued on `producer` so far (ints)."""
     check(lib.dgs_stream_wait(ctypes.c_void_p(producer), ctypes.c_void_p(consumer)))

@@ -181,6 +181,14 @@ int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_see
                              int64_t *const *cols, const uint64_t *launch_seeds, int flags,
                              void *stream);
 int dgs_sampler_sample_end(dgs_sampler *s, int L, int64_t *sizes_out, void *stream);
+/* ADDITIVE: `stream` first waits for the work enqueued on `wait_for` so far (when non-NULL),
+ * then dgs_sampler_sample_begin -- one call per batch for a pipelined loader.  `seeds` must be
+ * device memory (no pointer-attribute query). */
+int dgs_sampler_sample_begin_after(dgs_sampler *s, void *wait_for, const int64_t *seeds,
+                                   int64_t n_seeds, const int64_t *fan_out, int L, int replace,
+                                   int64_t *const *frontiers, int64_t *const *rows,
+                                   int64_t *const *cols, const uint64_t *launch_seeds, int flags,
+                                   void *stream);
 /* _CAPI_get_local_cache_structure_tensors (sampler.cc:183-195): non-owning device views. */
 int dgs_sampler_local_cache(const dgs_sampler *s, const int64_t **sub_indptr, int64_t *n_rows,
                             const int64_t **sub_indices, int64_t *n_edges,
@@ -209,6 +217,14 @@ int dgs_feature_server_gather(dgs_feature_server *s, const int64_t *nids, int64_
                               void *out, void *stream);
 int dgs_feature_server_local_cache(const dgs_feature_server *s, const void **ptr,
                                    int64_t *rows);
+/* ADDITIVE (PrefetchLoader, one call per batch): `consumer` waits for `producer` (the batch's
+ * sample call), then on `consumer` the feature gather of nids[n] into feat_out (fs may be
+ * NULL) and, when labels != NULL, label_out[i] = labels[seeds[i]] (rows of label_row_bytes,
+ * int64 seeds).  nids, seeds and every buffer are device memory. */
+int dgs_loader_gather(dgs_feature_server *fs, void *producer, void *consumer,
+                      const int64_t *nids, int64_t n, void *feat_out, const void *labels,
+                      int64_t label_row_bytes, const int64_t *seeds, int64_t n_seeds,
+                      void *label_out);
 /* ADDITIVE.  Address layout the gather uses: -1 = per-node address table (general cache
  * placement), w >= 0 = every node cached in the strided layout (node v at row v >> w of GPU
  * v & (2^w - 1); w = 0 is the whole-graph-in-HBM identity), no per-node table read. */

@@ -27,11 +27,14 @@ def main():
     p.add_argument("--steps", type=int, default=2000)
     p.add_argument("--scale", type=int, default=21)
     p.add_argument("--ef", type=int, default=59)
+    p.add_argument("--fan-out", type=str, default="15,10,5")
+    p.add_argument("--dim", type=int, default=100)
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     ip, ix = rmat_csc_torch(a.scale, a.ef, seed=20261015, device=dev)
     N = ip.numel() - 1
-    feats = torch.randn(N, 100, device=dev).cpu()
+    feats = torch.randn(N, a.dim, device=dev).cpu()
+    fan_out = [int(x) for x in a.fan_out.split(",")]
     labels = torch.randint(0, 47, (N,), device=dev)
     sampler = C.P2PCacheSampler(ip.cpu(), ix.cpu(), torch.Tensor(), torch.arange(N), 0)
     server = C.P2PCacheFeatureServer(feats, torch.arange(N), 0)
@@ -49,20 +52,20 @@ def main():
         finally:
             wait[0] += time.perf_counter() - t
 
-    for _ in PrefetchLoader(sampler, batches[:50], [15, 10, 5], server=server, labels=labels,
+    for _ in PrefetchLoader(sampler, batches[:50], fan_out, server=server, labels=labels,
                             depth=a.depth):
         pass
     torch.cuda.synchronize()
     C._PendingSample.result = timed
     t0 = time.perf_counter()
-    for _ in PrefetchLoader(sampler, batches, [15, 10, 5], server=server, labels=labels,
+    for _ in PrefetchLoader(sampler, batches, fan_out, server=server, labels=labels,
                             depth=a.depth):
         pass
     torch.cuda.synchronize()
     tot = time.perf_counter() - t0
     C._PendingSample.result = orig
     n = len(batches)
-    print(f"B={a.batch} depth={a.depth}: {tot / n * 1e6:.1f} us/batch total, "
+    print(f"B={a.batch} fan-out {fan_out} depth={a.depth}: {tot / n * 1e6:.1f} us/batch total, "
           f"{wait[0] / n * 1e6:.1f} us waiting for sizes, "
           f"{(tot - wait[0]) / n * 1e6:.1f} us host work")
 
