@@ -196,12 +196,15 @@ int dgs_stream_wait(void *producer, void *consumer) {
   return guard([&] { stream_wait_impl(producer, consumer); });
 }
 
-int dgs_loader_gather(dgs_feature_server *fs, void *producer, void *consumer,
+int dgs_loader_gather(dgs_sampler *s, dgs_feature_server *fs, void *producer, void *consumer,
                       const int64_t *nids, int64_t n, void *feat_out, const void *labels,
                       int64_t label_row_bytes, const int64_t *seeds, int64_t n_seeds,
                       void *label_out) {
   return guard([&] {
-    stream_wait_impl(producer, consumer);
+    if (s)
+      DGS_HIP(hipStreamWaitEvent(S(consumer), s->s->ended_event(S(producer)), 0));
+    else
+      stream_wait_impl(producer, consumer);
     if (fs && n > 0) fs->s->gather(nids, n, feat_out, S(consumer));
     if (labels && n_seeds > 0)
       gather_plain(labels, label_row_bytes, seeds, 8, n_seeds, label_out, S(consumer));

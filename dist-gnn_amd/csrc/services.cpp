@@ -176,6 +176,7 @@ Sampler::~Sampler() {
       c.launcher.join();
     }
     if (c.seq > 0) (void)hipStreamSynchronize(c.stream);  // the last relabel pass may still run
+    if (c.end_ev) (void)hipEventDestroy(c.end_ev);
   }
   delete indptr_srv_;
   delete indices_srv_;
@@ -364,6 +365,17 @@ void Sampler::launch(Ctx &c, const Job &j, hipStream_t st) {
     S = Count{fcap[h], d_uniq};
   }
   profile_end(st, 1);
+  // recorded here (on the launcher thread when the call is asynchronous), so a consumer of the
+  // outputs only needs a stream wait on the caller's thread (ended_event)
+  if (!c.end_ev) DGS_HIP(hipEventCreateWithFlags(&c.end_ev, hipEventDisableTiming));
+  DGS_HIP(hipEventRecord(c.end_ev, st));
+}
+
+hipEvent_t Sampler::ended_event(hipStream_t st) {
+  Ctx &c = ctx_for(st);
+  std::lock_guard<std::mutex> g(c.mu);
+  DGS_CHECK(!c.pending && c.end_ev, "ended_event: no ended call on this stream");
+  return c.end_ev;
 }
 
 // Waits for the sizes of the call begun on `st` (published by its last scatter kernel): the

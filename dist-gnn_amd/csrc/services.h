@@ -77,6 +77,10 @@ class Sampler {
                     int64_t *const *cols, hipStream_t st, const uint64_t *launch_seeds,
                     bool host_async = false);
   void sample_end(int L, int64_t *sizes, hipStream_t st);
+  // The event the last call on `st` recorded after its launches (valid once that call has been
+  // ended and until the next call on `st` is begun): a consumer stream waits on it without a
+  // record of its own on the caller's thread.
+  hipEvent_t ended_event(hipStream_t st);
   const int64_t *sub_indptr() const { return (const int64_t *)indptr_srv_->local(); }
   int64_t n_rows() const { return indptr_srv_->items(rank_) - 1; }
   const int64_t *sub_indices() const { return (const int64_t *)indices_srv_->local(); }
@@ -126,6 +130,7 @@ class Sampler {
     bool pending = false;  // a call was begun and not yet ended
     int pending_L = 0;
     int64_t pending_seeds = 0;
+    hipEvent_t end_ev = nullptr;  // recorded on the stream after each call's launches
   };
   Ctx &ctx_for(hipStream_t st);
   void launch(Ctx &c, const Job &j, hipStream_t st);

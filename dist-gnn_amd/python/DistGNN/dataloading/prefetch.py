@@ -147,8 +147,9 @@ class PrefetchLoader:
         if self.labels is not None:
             y = torch.empty((s64.numel(),) + tuple(self.labels.shape[1:]),
                             dtype=self.labels.dtype, device=self.device)
-        dgs.ops._loader_gather(self.server, st, cur, front, x, self.labels,
-                               self._label_row_bytes, s64, y)
+        # (the sampler's launches recorded the event this wait uses: no record here)
+        dgs.ops._loader_gather(self.sampler if blocks else None, self.server, st, cur, front, x,
+                               self.labels, self._label_row_bytes, s64, y)
         dt = self.sampler._id_dtype
         if dt != torch.int64:  # int32 graphs: cast on the caller's stream, now ordered after B
             cast, cur_seeds = [], blocks[0][0]

@@ -129,7 +129,7 @@ class P2PCacheSampler:
         if L and launch_seeds is not None:
             ls = (ctypes.c_uint64 * L)(*[int(x) & 0xFFFFFFFFFFFFFFFF for x in launch_seeds])
         if L and wait_for is not None:
-            check(lib.dgs_sampler_sample_begin_after(self._h, c_vp(wait_for), c_vp(s.data_ptr()),
+            check(lib.dgs_sampler_sample_begin_after(self._h, wait_for, s.data_ptr(),
                                                      s.numel(), fo, L, int(bool(replace)), *ptrs,
                                                      ls, 1 if host_async else 0, st))
         elif L:

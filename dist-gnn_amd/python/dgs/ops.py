@@ -235,18 +235,20 @@ def _index_select_into(data, nid, out, stream):
                                       ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))
 
 
-def _loader_gather(server, producer, consumer, nids, x, labels, label_row_bytes, seeds, y):
-    """ADDITIVE (PrefetchLoader): `consumer` waits for `producer`, then x = features[nids]
-    (server may be None) and y = labels[seeds] (labels may be None), on `consumer`; one C-ABI
-    call.  All tensors contiguous device tensors, nids and seeds int64."""
-    vp = ctypes.c_void_p
+def _loader_gather(sampler, server, producer, consumer, nids, x, labels, label_row_bytes, seeds,
+                   y):
+    """ADDITIVE (PrefetchLoader): `consumer` waits for `producer` (the sample call of
+    `sampler` just ended on it; sampler None: any work), then x = features[nids] (server may be
+    None) and y = labels[seeds] (labels may be None), on `consumer`; one C-ABI call.  All
+    tensors contiguous device tensors, nids and seeds int64; streams are ints."""
     check(lib.dgs_loader_gather(
-        server._h if server is not None else None, vp(producer), vp(consumer),
-        vp(nids.data_ptr()) if nids is not None else None,
-        nids.numel() if nids is not None else 0, vp(x.data_ptr()) if x is not None else None,
-        vp(labels.data_ptr()) if labels is not None else None, int(label_row_bytes),
-        vp(seeds.data_ptr()), seeds.numel() if labels is not None else 0,
-        vp(y.data_ptr()) if y is not None else None))
+        sampler._h if sampler is not None else None,
+        server._h if server is not None else None, producer, consumer,
+        nids.data_ptr() if nids is not None else None, nids.numel() if nids is not None else 0,
+        x.data_ptr() if x is not None else None,
+        labels.data_ptr() if labels is not None else None, label_row_bytes,
+        seeds.data_ptr(), seeds.numel() if labels is not None else 0,
+        y.data_ptr() if y is not None else None))
 
 
 def _stream_wait(producer, consumer):

@@ -220,8 +220,11 @@ int dgs_feature_server_local_cache(const dgs_feature_server *s, const void **ptr
 /* ADDITIVE (PrefetchLoader, one call per batch): `consumer` waits for `producer` (the batch's
  * sample call), then on `consumer` the feature gather of nids[n] into feat_out (fs may be
  * NULL) and, when labels != NULL, label_out[i] = labels[seeds[i]] (rows of label_row_bytes,
- * int64 seeds).  nids, seeds and every buffer are device memory. */
-int dgs_loader_gather(dgs_feature_server *fs, void *producer, void *consumer,
+ * int64 seeds).  nids, seeds and every buffer are device memory.  With s != NULL the call on
+ * `producer` must have been ended (dgs_sampler_sample_end) and no new one begun: `consumer`
+ * waits on the event that call's launches recorded, with no event record here; with s == NULL
+ * an event is recorded on `producer` now. */
+int dgs_loader_gather(dgs_sampler *s, dgs_feature_server *fs, void *producer, void *consumer,
                       const int64_t *nids, int64_t n, void *feat_out, const void *labels,
                       int64_t label_row_bytes, const int64_t *seeds, int64_t n_seeds,
                       void *label_out);
