@@ -400,14 +400,24 @@ int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_see
 
 int dgs_sampler_sample_begin_after(dgs_sampler *s, void *wait_for, const int64_t *seeds,
                                    int64_t n_seeds, const int64_t *fan_out, int L, int replace,
-                                   int64_t *const *frontiers, int64_t *const *rows,
-                                   int64_t *const *cols, const uint64_t *launch_seeds, int flags,
+                                   int64_t *out, const uint64_t *launch_seeds, int flags,
                                    void *stream) {
   return guard([&] {
     DGS_CHECK((flags & ~DGS_SAMPLE_HOST_ASYNC) == 0, "sample_begin: unknown flags");
+    DGS_CHECK(L > 0 && L <= 64, "sample_begin: 1 to 64 hops");
+    int64_t fcap[64], ecap[64];
+    int64_t *fr[64], *rows[64], *cols[64];
+    s->s->bounds(n_seeds, fan_out, L, fcap, ecap);
+    int64_t *p = out;  // per hop: frontier[fcap], rows[ecap], cols[ecap]
+    for (int h = 0; h < L; ++h) {
+      fr[h] = p;
+      rows[h] = p + fcap[h];
+      cols[h] = p + fcap[h] + ecap[h];
+      p += fcap[h] + 2 * ecap[h];
+    }
     if (wait_for) stream_wait_impl(wait_for, stream);
-    s->s->sample_begin(seeds, n_seeds, fan_out, L, replace != 0, frontiers, rows, cols,
-                       S(stream), launch_seeds, (flags & DGS_SAMPLE_HOST_ASYNC) != 0);
+    s->s->sample_begin(seeds, n_seeds, fan_out, L, replace != 0, fr, rows, cols, S(stream),
+                       launch_seeds, (flags & DGS_SAMPLE_HOST_ASYNC) != 0);
   });
 }
 

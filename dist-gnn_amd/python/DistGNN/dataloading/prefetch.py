@@ -108,7 +108,8 @@ class PrefetchLoader:
         cur = self._caller_stream()
         # the caller may drop its seeds at once: their memory must outlive B's reads
         seeds.record_stream(self._streams[w])
-        prep = self.sampler._prepare(seeds, self.fan_out)  # int64 seeds + outputs, on C
+        # int64 seeds + one output buffer, on C
+        prep = self.sampler._prepare(seeds, self.fan_out, packed=True)
         # B waits for C (after the allocations), then the call is enqueued: one C-ABI call.
         # B is not touched again before result(): the sampler's launcher thread may issue
         # the launches.  The sampler draws the launch seeds once it has accepted the call.

@@ -68,8 +68,7 @@ _SIGS = {
                                          p_vp, ctypes.POINTER(c_u64), c_int, c_vp]),
     "dgs_sampler_sample_end": (c_int, [c_vp, c_int, p_i64, c_vp]),
     "dgs_sampler_sample_begin_after": (c_int, [c_vp, c_vp, c_vp, c_i64, p_i64, c_int, c_int,
-                                               p_vp, p_vp, p_vp, ctypes.POINTER(c_u64), c_int,
-                                               c_vp]),
+                                               c_vp, ctypes.POINTER(c_u64), c_int, c_vp]),
     "dgs_loader_gather": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                   c_i64, c_vp]),
     "dgs_sampler_local_cache": (c_int, [c_vp, p_vp, p_i64, p_vp, p_i64, p_vp]),

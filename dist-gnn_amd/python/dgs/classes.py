@@ -130,8 +130,9 @@ class P2PCacheSampler:
             ls = (ctypes.c_uint64 * L)(*[int(x) & 0xFFFFFFFFFFFFFFFF for x in launch_seeds])
         if L and wait_for is not None:
             check(lib.dgs_sampler_sample_begin_after(self._h, wait_for, s.data_ptr(),
-                                                     s.numel(), fo, L, int(bool(replace)), *ptrs,
-                                                     ls, 1 if host_async else 0, st))
+                                                     s.numel(), fo, L, int(bool(replace)),
+                                                     buf.data_ptr(), ls, 1 if host_async else 0,
+                                                     st))
         elif L:
             check(lib.dgs_sampler_sample_begin(self._h, c_vp(s.data_ptr()), s.numel(), fo, L,
                                                int(bool(replace)), *ptrs, ls,
@@ -151,7 +152,8 @@ class P2PCacheSampler:
                                      int(bool(replace)), *ptrs, sizes, stream_ptr(s.device)))
         return self._views(seeds, buf, caps, total, sizes, L)
 
-    def _prepare(self, seeds, fan_out):
+    def _prepare(self, seeds, fan_out, packed=False):
+        """packed: no per-hop pointer arrays (the buffer goes to the C ABI whole)."""
         check_cuda(seeds, "seeds")
         s = seeds if seeds.dtype == torch.int64 and seeds.is_contiguous() else \
             as_i64(seeds, "seeds")
@@ -170,7 +172,7 @@ class P2PCacheSampler:
         fo, caps, total = plan
         # one allocation for every hop's (frontier, row, col) buffers
         buf = torch.empty(max(total, 1), dtype=torch.int64, device=s.device)
-        return s, L, fo, caps, total, buf, plan_ptrs(buf.data_ptr(), caps)
+        return s, L, fo, caps, total, buf, None if packed else plan_ptrs(buf.data_ptr(), caps)
 
     def _views(self, seeds, buf, caps, total, sizes, L, cast=True):
         # all views in one split: [U_h, pad, nnz_h, pad, nnz_h, pad] per hop

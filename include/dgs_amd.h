@@ -182,12 +182,13 @@ int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_see
                              void *stream);
 int dgs_sampler_sample_end(dgs_sampler *s, int L, int64_t *sizes_out, void *stream);
 /* ADDITIVE: `stream` first waits for the work enqueued on `wait_for` so far (when non-NULL),
- * then dgs_sampler_sample_begin -- one call per batch for a pipelined loader.  `seeds` must be
- * device memory (no pointer-attribute query). */
+ * then dgs_sampler_sample_begin with every hop's outputs packed in one device buffer `out`:
+ * per hop h, frontier[fcap_h], rows[ecap_h], cols[ecap_h] back to back (the capacities of
+ * dgs_sampler_bounds) -- one call per batch for a pipelined loader.  `seeds` must be device
+ * memory (no pointer-attribute query); 1 <= L <= 64. */
 int dgs_sampler_sample_begin_after(dgs_sampler *s, void *wait_for, const int64_t *seeds,
                                    int64_t n_seeds, const int64_t *fan_out, int L, int replace,
-                                   int64_t *const *frontiers, int64_t *const *rows,
-                                   int64_t *const *cols, const uint64_t *launch_seeds, int flags,
+                                   int64_t *out, const uint64_t *launch_seeds, int flags,
                                    void *stream);
 /* _CAPI_get_local_cache_structure_tensors (sampler.cc:183-195): non-owning device views. */
 int dgs_sampler_local_cache(const dgs_sampler *s, const int64_t **sub_indptr, int64_t *n_rows,
