@@ -205,8 +205,22 @@ int dgs_loader_gather(dgs_sampler *s, dgs_feature_server *fs, void *producer, vo
       DGS_HIP(hipStreamWaitEvent(S(consumer), s->s->ended_event(S(producer)), 0));
     else
       stream_wait_impl(producer, consumer);
-    if (fs && n > 0) fs->s->gather(nids, n, feat_out, S(consumer));
-    if (labels && n_seeds > 0)
+    const bool want_labels = labels && n_seeds > 0;
+    // 4- and 8-byte label rows ride in the feature gather's launch
+    const bool fuse = want_labels && fs && n > 0 && n_seeds < (int64_t(1) << 31) &&
+                      (label_row_bytes == 4 || label_row_bytes == 8) &&
+                      ((uintptr_t)labels % label_row_bytes) == 0 &&
+                      ((uintptr_t)label_out % label_row_bytes) == 0;
+    LabelTail lt;
+    if (fuse) {
+      lt.data = (const char *)labels;
+      lt.ids = seeds;
+      lt.out = (char *)label_out;
+      lt.n = (uint32_t)n_seeds;
+      lt.row_bytes = (uint32_t)label_row_bytes;
+    }
+    if (fs && n > 0) fs->s->gather(nids, n, feat_out, S(consumer), fuse ? &lt : nullptr);
+    if (want_labels && !fuse)
       gather_plain(labels, label_row_bytes, seeds, 8, n_seeds, label_out, S(consumer));
   });
 }

@@ -9,18 +9,31 @@
 namespace dgs {
 
 // ---------------------------------------------------------------- gather (gather.hip)
+// A second, small gather fused into a feature gather's launch (PrefetchLoader's label gather):
+// out[i] = data[ids[i]] for i < n, rows of 4 or 8 bytes, in extra workgroups after the
+// feature gather's (one launch instead of two on the caller's thread).
+struct LabelTail {
+  const char *data = nullptr;
+  const int64_t *ids = nullptr;
+  char *out = nullptr;
+  uint32_t n = 0;
+  uint32_t row_bytes = 0;  // 4 or 8
+  uint32_t blk0 = 0xffffffffu;  // first label workgroup (set by the launcher)
+};
 // out[i, :] = data[nid[i], :], a row_bytes byte copy per row.
 void gather_plain(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
                   int64_t n, void *out, hipStream_t st);
 // out[i, :] = *(row_bytes at ftab[nids[i]]): ftab holds the absolute (device-accessible)
 // address of every node's feature row.  align_or = OR of all row base addresses.
 void gather_table(const int64_t *ftab, uintptr_t align_or, int64_t row_bytes,
-                  const int64_t *nids, int64_t n, void *out, hipStream_t st);
+                  const int64_t *nids, int64_t n, void *out, hipStream_t st,
+                    const LabelTail *tail = nullptr);
 // Strided cache layout (every node cached, node v at row v >> wshift of GPU v & (W - 1),
 // W = 1 << wshift <= 8; W = 1 is the whole-graph-in-HBM identity layout): the row address is
 // computed, so the gather reads no per-node table.  bases[d] = GPU d's (IPC-mapped) block.
 void gather_strided(const void *const *bases, int wshift, int64_t row_bytes,
-                    const int64_t *nids, int64_t n, void *out, hipStream_t st);
+                    const int64_t *nids, int64_t n, void *out, hipStream_t st,
+                    const LabelTail *tail = nullptr);
 // number of i < n with list[i] != start + i * stride (device count -> host)
 int64_t count_stride_mismatch(const int64_t *list, int64_t n, int64_t start, int64_t stride,
                               hipStream_t st);

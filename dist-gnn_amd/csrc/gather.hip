@@ -152,13 +152,26 @@ template <int V, typename Src>
 __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nchunks,
                                                            uint32_t cpr, FastDivU32 fd,
                                                            char *__restrict__ out,
-                                                           uint64_t *stamp) {
+                                                           uint64_t *stamp, LabelTail lt) {
   using T = typename VecT<V>::T;
 #if DGS_GATHER_PRIO
   // issue priority over co-resident waves of other kernels (the sampler's VALU-bound waves
   // share the SIMDs in the pipeline): this wave's loads and stores go out first
   __builtin_amdgcn_s_setprio(DGS_GATHER_PRIO);
 #endif
+  if (blockIdx.x >= lt.blk0) {  // fused label rows (uniform branch), one per lane
+    const uint32_t i = (blockIdx.x - lt.blk0) * (uint32_t)kGatherThreads + threadIdx.x;
+    if (i < lt.n) {
+      const int64_t id = lt.ids[i];
+      if (lt.row_bytes == 8)
+        reinterpret_cast<uint64_t *>(lt.out)[i] =
+            *to_global<uint64_t>(lt.data + (size_t)id * 8);
+      else
+        reinterpret_cast<uint32_t *>(lt.out)[i] =
+            *to_global<uint32_t>(lt.data + (size_t)id * 4);
+    }
+    return;
+  }
   // profiling only (stamp != nullptr, a kernel argument: uniform branch)
   if (stamp && threadIdx.x == 0) stamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   const uint32_t base = blockIdx.x * (uint32_t)(kGatherThreads * kGatherUnroll) + threadIdx.x;
@@ -200,7 +213,7 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nch
 
 template <typename Src>
 void launch_gather_v(int V, Src src, int64_t n, int64_t row_bytes, char *out, hipStream_t st,
-                     int which) {
+                     int which, const LabelTail *tail = nullptr) {
   const int64_t cpr = row_bytes / V;
   DGS_CHECK(cpr > 0 && cpr < (int64_t(1) << 30), "gather: unsupported row size");
   const int64_t max_rows = ((int64_t(1) << 31) - kGatherThreads * kGatherUnroll) / cpr;
@@ -210,17 +223,24 @@ void launch_gather_v(int V, Src src, int64_t n, int64_t row_bytes, char *out, hi
     Src s = src;
     s.row_base = r0;
     const uint32_t nchunks = (uint32_t)(rows * cpr);
-    const dim3 grid((unsigned)ceil_div(nchunks, kGatherThreads * kGatherUnroll));
+    dim3 grid((unsigned)ceil_div(nchunks, kGatherThreads * kGatherUnroll));
     char *o = out + r0 * row_bytes;
+    // stamps cover the feature workgroups only (the label workgroups return before stamping)
     uint64_t *stamp = profile_stamps(which, (int64_t)grid.x);
+    LabelTail lt;
+    if (tail && r0 == 0 && tail->n > 0) {
+      lt = *tail;
+      lt.blk0 = grid.x;
+      grid.x += (unsigned)ceil_div((int64_t)lt.n, kGatherThreads);
+    }
     const dim3 block(kGatherThreads);
     const uint32_t c32 = (uint32_t)cpr;
     switch (V) {
-      case 16: hipLaunchKernelGGL((k_gather<16, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp); break;
-      case 8: hipLaunchKernelGGL((k_gather<8, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp); break;
-      case 4: hipLaunchKernelGGL((k_gather<4, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp); break;
-      case 2: hipLaunchKernelGGL((k_gather<2, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp); break;
-      default: hipLaunchKernelGGL((k_gather<1, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp); break;
+      case 16: hipLaunchKernelGGL((k_gather<16, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt); break;
+      case 8: hipLaunchKernelGGL((k_gather<8, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt); break;
+      case 4: hipLaunchKernelGGL((k_gather<4, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt); break;
+      case 2: hipLaunchKernelGGL((k_gather<2, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt); break;
+      default: hipLaunchKernelGGL((k_gather<1, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt); break;
     }
     DGS_LAUNCH_CHECK();
   }
@@ -260,15 +280,17 @@ void gather_plain(const void *data, int64_t row_bytes, const void *nid, int nid_
 }
 
 void gather_table(const int64_t *ftab, uintptr_t align_or, int64_t row_bytes,
-                  const int64_t *nids, int64_t n, void *out, hipStream_t st) {
+                  const int64_t *nids, int64_t n, void *out, hipStream_t st,
+                  const LabelTail *tail) {
   if (n <= 0 || row_bytes <= 0) return;
   const int V = pick_vec(row_bytes, align_or | (uintptr_t)out);
   TableSrc s{ftab, nids, row_bytes, 0};
-  launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0);
+  launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0, tail);
 }
 
 void gather_strided(const void *const *bases, int wshift, int64_t row_bytes,
-                    const int64_t *nids, int64_t n, void *out, hipStream_t st) {
+                    const int64_t *nids, int64_t n, void *out, hipStream_t st,
+                    const LabelTail *tail) {
   if (n <= 0 || row_bytes <= 0) return;
   DGS_CHECK(wshift >= 0 && wshift <= 3, "strided gather: at most 8 locations");
   const int W = 1 << wshift;
@@ -281,11 +303,11 @@ void gather_strided(const void *const *bases, int wshift, int64_t row_bytes,
   const int V = pick_vec(row_bytes, align_or);
   if (wshift == 0) {
     StridedSrc<false> s{nids, b[0], b[1], b[2], b[3], b[4], b[5], b[6], b[7], row_bytes, 0, 0};
-    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0);
+    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0, tail);
   } else {
     StridedSrc<true> s{nids, b[0], b[1], b[2], b[3], b[4], b[5], b[6], b[7], row_bytes, 0,
                        (uint32_t)wshift};
-    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0);
+    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0, tail);
   }
 }
 

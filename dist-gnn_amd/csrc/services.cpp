@@ -528,11 +528,12 @@ void FeatureServer::detect_strided(const std::vector<void *> &lists,
 
 FeatureServer::~FeatureServer() { delete feat_srv_; }
 
-void FeatureServer::gather(const int64_t *nids, int64_t n, void *out, hipStream_t st) const {
+void FeatureServer::gather(const int64_t *nids, int64_t n, void *out, hipStream_t st,
+                           const LabelTail *tail) const {
   if (wshift_ >= 0)
-    gather_strided(bases_, wshift_, row_bytes_, nids, n, out, st);
+    gather_strided(bases_, wshift_, row_bytes_, nids, n, out, st, tail);
   else
-    gather_table(ftab_.as<int64_t>(), align_or_, row_bytes_, nids, n, out, st);
+    gather_table(ftab_.as<int64_t>(), align_or_, row_bytes_, nids, n, out, st, tail);
 }
 
 }  // namespace dgs

@@ -144,7 +144,9 @@ class FeatureServer {
   FeatureServer(const void *data, int64_t num_rows, int64_t row_bytes, const int64_t *cache_nids,
                 int64_t n_cache, int64_t device_id);
   ~FeatureServer();
-  void gather(const int64_t *nids, int64_t n, void *out, hipStream_t st) const;
+  // tail: a label gather fused into the same launch (n > 0 only)
+  void gather(const int64_t *nids, int64_t n, void *out, hipStream_t st,
+              const LabelTail *tail = nullptr) const;
   const void *local() const { return feat_srv_ ? feat_srv_->local() : nullptr; }
   int64_t local_rows() const { return feat_srv_ ? feat_srv_->items(rank_) : 0; }
   int layout() const { return wshift_; }

@@ -279,3 +279,26 @@ def test_loader_streams_are_returned(dgs):
     second.close()
     dev = torch.device("cuda", torch.cuda.current_device())
     assert len(P._FREE_STREAMS[dev]) >= 4
+
+
+@pytest.mark.parametrize("kind", ["int64", "int32", "float32", "int64x3", "no_server"])
+def test_prefetch_label_rows(dgs, kind):
+    """The label gather rides in the feature gather's launch for 4- and 8-byte label rows
+    (dgs_loader_gather); wider rows and server-less loaders take the separate gather."""
+    from DistGNN.dataloading import PrefetchLoader
+    _, sampler, server, labels, feats = _services(dgs, False)
+    base = labels.long()
+    lab = {"int64": base, "int32": base.int(), "float32": base.float() * 0.5 + 0.25,
+           "int64x3": torch.stack([base, base * 3, -base], 1),
+           "no_server": base}[kind]
+    srv = None if kind == "no_server" else server
+    batches = _batches(base.numel(), nb=6)
+    got = list(PrefetchLoader(sampler, batches, [5, 3], server=srv, labels=lab, depth=3))
+    torch.cuda.synchronize()
+    lab_d = lab.to(batches[0].device)
+    for s, (blocks, x, y) in zip(batches, got):
+        assert y.dtype == lab.dtype and torch.equal(y, lab_d[s.long()])
+        if srv is None:
+            assert x is None
+        else:
+            assert torch.equal(x.cpu(), feats[blocks[-1][1].long().cpu()])
