@@ -5,6 +5,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 #include "dgs_ops.h"
 
@@ -135,9 +137,59 @@ bool is_device_pointer(const void *p) {
          a.type == hipMemoryTypeUnified;
 }
 
+namespace {
+// Host ranges this library registered, with the number of live views into each: two services
+// over one host tensor share its registration, and the range is unregistered when the last of
+// them goes (unregistering it with the first would unmap the other's device view).
+struct HostReg {
+  size_t bytes;
+  int refs;
+};
+std::mutex &host_reg_mu() {
+  static std::mutex m;
+  return m;
+}
+std::map<uintptr_t, HostReg> &host_regs() {
+  static std::map<uintptr_t, HostReg> m;
+  return m;
+}
+// the registered range holding p (caller holds the lock), or end()
+std::map<uintptr_t, HostReg>::iterator host_reg_find(const void *p) {
+  auto &m = host_regs();
+  const uintptr_t x = (uintptr_t)p;
+  auto it = m.upper_bound(x);
+  if (it == m.begin()) return m.end();
+  --it;
+  return x < it->first + it->second.bytes ? it : m.end();
+}
+}  // namespace
+
+void release_host_view(const void *p) {
+  std::lock_guard<std::mutex> g(host_reg_mu());
+  auto it = host_reg_find(p);
+  if (it == host_regs().end()) return;
+  if (--it->second.refs == 0) {
+    (void)hipHostUnregister(reinterpret_cast<void *>(it->first));
+    host_regs().erase(it);
+  }
+}
+
 void *device_view(const void *p, int64_t bytes, bool *registered_here) {
   if (registered_here) *registered_here = false;
   if (!p) return nullptr;
+  std::lock_guard<std::mutex> g(host_reg_mu());
+  {
+    auto it = host_reg_find(p);
+    if (it != host_regs().end() && (uintptr_t)p + (size_t)(bytes > 0 ? bytes : 1) <=
+                                       it->first + it->second.bytes) {
+      // a range registered here already: share it
+      void *d = nullptr;
+      DGS_HIP(hipHostGetDevicePointer(&d, reinterpret_cast<void *>(it->first), 0));
+      ++it->second.refs;
+      if (registered_here) *registered_here = true;
+      return static_cast<char *>(d) + ((uintptr_t)p - it->first);
+    }
+  }
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) == hipSuccess) {
     if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
@@ -153,11 +205,16 @@ void *device_view(const void *p, int64_t bytes, bool *registered_here) {
     (void)hipGetLastError();
   }
   // pageable host memory: register it (mapped) for zero-copy device reads
-  DGS_HIP(hipHostRegister(const_cast<void *>(p), (size_t)(bytes > 0 ? bytes : 1),
-                          hipHostRegisterMapped));
-  if (registered_here) *registered_here = true;
+  const size_t nb = (size_t)(bytes > 0 ? bytes : 1);
+  DGS_HIP(hipHostRegister(const_cast<void *>(p), nb, hipHostRegisterMapped));
   void *d = nullptr;
-  DGS_HIP(hipHostGetDevicePointer(&d, const_cast<void *>(p), 0));
+  const hipError_t e = hipHostGetDevicePointer(&d, const_cast<void *>(p), 0);
+  if (e != hipSuccess) {
+    (void)hipHostUnregister(const_cast<void *>(p));
+    DGS_HIP(e);
+  }
+  host_regs()[(uintptr_t)p] = HostReg{nb, 1};
+  if (registered_here) *registered_here = true;
   return d;
 }
 

@@ -81,7 +81,10 @@ class Comm {
 // Device-accessible pointer for `p`: device memory is returned as is; pinned / registered
 // host memory is translated; pageable host memory is registered (mapped) first and
 // *registered_here is set so the owner can unregister it.
+// *registered_here = true: the view holds a reference on a registration made by this library
+// (shared by every view into the range); release it with release_host_view(p).
 void *device_view(const void *p, int64_t bytes, bool *registered_here);
+void release_host_view(const void *p);
 bool is_device_pointer(const void *p);
 
 }  // namespace dgs

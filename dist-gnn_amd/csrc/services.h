@@ -53,7 +53,7 @@ struct HostView {
     dev = device_view(p, bytes, &registered_here);
   }
   ~HostView() {
-    if (registered_here) (void)hipHostUnregister(const_cast<void *>(host));
+    if (registered_here) release_host_view(host);
   }
 };
 

@@ -464,3 +464,26 @@ def test_standalone_ops_on_two_streams(dgs):
     for g, e in zip(got_o, exp_o):
         for a, b in zip(g, e):
             assert torch.equal(a, b)
+
+
+def test_shared_host_registration_outlives_first_owner(dgs):
+    """Two services over one pageable host tensor share the library's registration of it: the
+    first one's destruction must not unmap the second's device view (refcounted registry)."""
+    import gc
+    rng = np.random.default_rng(4)
+    data = torch.from_numpy(rng.standard_normal((2000, 64)).astype(np.float32))
+    assert not data.is_pinned()
+    a = dgs.classes.P2PCacheFeatureServer(data, torch.tensor([5]), 0)
+    b = dgs.classes.P2PCacheFeatureServer(data, torch.tensor([9]), 0)
+    q = rng.integers(0, 2000, 4096)
+    exp = O.index_select(data.numpy(), q)
+    assert np.array_equal(a._CAPI_get_feature(_cuda(q)).cpu().numpy(), exp)
+    del a
+    gc.collect()
+    torch.cuda.synchronize()
+    assert np.array_equal(b._CAPI_get_feature(_cuda(q)).cpu().numpy(), exp)
+    del b
+    gc.collect()
+    # all views gone: the range is unregistered, a new service registers it again
+    c = dgs.classes.P2PCacheFeatureServer(data, torch.tensor([1]), 0)
+    assert np.array_equal(c._CAPI_get_feature(_cuda(q)).cpu().numpy(), exp)

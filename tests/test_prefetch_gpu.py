@@ -302,3 +302,20 @@ def test_prefetch_label_rows(dgs, kind):
             assert x is None
         else:
             assert torch.equal(x.cpu(), feats[blocks[-1][1].long().cpu()])
+
+
+def test_prefetch_submit_error_surfaces_once(dgs):
+    """A batch that cannot be submitted (host seeds) fails the call that would submit it, after
+    the batches before it came out; the loader can still be closed."""
+    from DistGNN.dataloading import PrefetchLoader
+    _, sampler, server, labels, _ = _services(dgs, False)
+    batches = _batches(labels.numel(), nb=5)
+    batches[3] = batches[3].cpu()
+    it = PrefetchLoader(sampler, batches, [5, 5], server=server, depth=2)
+    for _ in range(2):
+        next(it)
+    with pytest.raises(RuntimeError):  # the call that submits batch 3
+        next(it)
+    it.close()
+    with pytest.raises(StopIteration):
+        next(it)
