@@ -167,14 +167,17 @@ int dgs_set_random_seed(uint64_t seed) {
 int dgs_host_register(void *ptr, int64_t bytes) {
   return guard([&] {
     if (!ptr || bytes <= 0) return;
-    DGS_HIP(hipHostRegister(ptr, (size_t)bytes, hipHostRegisterMapped));
+    // through the library's refcounted registry, shared with the services' host views
+    bool ref = false;
+    (void)device_view(ptr, bytes, &ref);
+    DGS_CHECK(ref, "host_register: the memory is already pinned outside this library");
   });
 }
 
 int dgs_host_unregister(void *ptr) {
   return guard([&] {
     if (!ptr) return;
-    DGS_HIP(hipHostUnregister(ptr));
+    release_host_view(ptr);
   });
 }
 

@@ -70,6 +70,10 @@ int dgs_set_random_seed(uint64_t seed);
 /* ------------------------------------------------------------------------------------
  * Host memory registration (src/common/pin_memory.cc:7-19; pybind.cc:57-58)
  * ---------------------------------------------------------------------------------- */
+/* Registrations are reference counted and shared with the host views of the services (a
+ * sampler or feature server over pageable host memory registers it the same way): unregister
+ * drops this call's reference, and the range is unmapped when the last reference goes.
+ * Memory pinned outside this library (hipHostMalloc, torch pin_memory) is refused. */
 int dgs_host_register(void *ptr, int64_t bytes);
 int dgs_host_unregister(void *ptr);
 

@@ -487,3 +487,18 @@ def test_shared_host_registration_outlives_first_owner(dgs):
     # all views gone: the range is unregistered, a new service registers it again
     c = dgs.classes.P2PCacheFeatureServer(data, torch.tensor([1]), 0)
     assert np.array_equal(c._CAPI_get_feature(_cuda(q)).cpu().numpy(), exp)
+
+
+def test_unpin_keeps_a_live_service_mapped(dgs):
+    """_CAPI_tensor_pin_memory / unpin share the services' refcounted registrations: unpinning a
+    tensor a feature server still reads leaves the server's view mapped."""
+    import gc
+    rng = np.random.default_rng(6)
+    data = torch.from_numpy(rng.standard_normal((1500, 32)).astype(np.float32))
+    dgs.ops._CAPI_tensor_pin_memory(data)
+    fs = dgs.classes.P2PCacheFeatureServer(data, torch.tensor([3]), 0)
+    dgs.ops._CAPI_tensor_unpin_memory(data)
+    gc.collect()
+    q = rng.integers(0, 1500, 2048)
+    assert np.array_equal(fs._CAPI_get_feature(_cuda(q)).cpu().numpy(),
+                          O.index_select(data.numpy(), q))
