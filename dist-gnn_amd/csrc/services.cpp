@@ -1,6 +1,8 @@
 // services.cpp -- TensorP2PServer, P2PCacheSampler, P2PCacheFeatureServer.
 #include "services.h"
 
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 namespace dgs {
@@ -276,6 +278,7 @@ void Sampler::sample_begin(const int64_t *seeds, int64_t n_seeds, const int64_t 
   }
   c.job = std::move(j);
   c.job_ready = true;
+  c.job_flag.store(true, std::memory_order_release);
   c.job_done = false;
   c.job_err = nullptr;
   c.cv.notify_all();
@@ -283,11 +286,30 @@ void Sampler::sample_begin(const int64_t *seeds, int64_t n_seeds, const int64_t 
 
 void Sampler::launcher_loop(Ctx &c, int dev) {
   (void)hipSetDevice(dev);
+  // Spin up to DGS_LAUNCHER_SPIN_US (default 1000; 0 = off) for the next job before sleeping on
+  // the condition variable: a sleeping thread's wake-up delays the batch's first launch (same
+  // box: biased pipeline +2 %, arxiv-like loader 35.5 -> 31.9 us/batch, 20 steps +1 %).
+  static const int64_t spin_ns = [] {
+    const char *e = std::getenv("DGS_LAUNCHER_SPIN_US");
+    return (e ? (int64_t)std::atoll(e) : (int64_t)1000) * 1000;
+  }();
   std::unique_lock<std::mutex> lk(c.mu);
   for (;;) {
+    if (spin_ns > 0 && !c.job_ready && !c.stop) {
+      lk.unlock();
+      const auto t0 = std::chrono::steady_clock::now();
+      for (uint32_t i = 1; !c.job_flag.load(std::memory_order_acquire); ++i) {
+        __builtin_ia32_pause();
+        if ((i & 63) == 0 && std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                 std::chrono::steady_clock::now() - t0).count() > spin_ns)
+          break;
+      }
+      lk.lock();
+    }
     c.cv.wait(lk, [&] { return c.job_ready || c.stop; });
     if (c.stop) return;
     c.job_ready = false;
+    c.job_flag.store(false, std::memory_order_relaxed);
     Job j = std::move(c.job);
     lk.unlock();
     std::exception_ptr err;

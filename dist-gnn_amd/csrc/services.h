@@ -4,6 +4,7 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <exception>
 #include <memory>
@@ -118,6 +119,7 @@ class Sampler {
     std::thread launcher;  // started by the first host-asynchronous call
     Job job;
     bool job_ready = false, job_done = true, stop = false;
+    std::atomic<bool> job_flag{false};  // job_ready, readable without the lock (launcher spin)
     std::exception_ptr job_err;
     HopScratch ws;
     DevBuf dpair[2];  // direct relabel tables over node ids ((first position, label) pairs),
