@@ -1,25 +1,42 @@
 """Benchmark of the DGS-AMD hot path (BASELINE.json metric: sampled edges/sec + feature-gather
-GB/s, fan-out [15,10,5]).
+GB/s, fan-out [15,10,5], 1/2/4/8 GPUs).
 
 One step = one training-loop data pass of the reference (example/graphsage/
 node_classification.py:219-229): P2PCacheSampler._CAPI_sample_node_classifiction(seeds,
 [15,10,5]) + P2PCacheFeatureServer._CAPI_get_feature(input nodes) +
-ops._CAPI_cuda_index_select(labels, seeds), on a synthetic products-like RMAT graph (configs[1]:
-uniform sampler + full-feature gather, d = 100, whole graph in HBM).  Inputs are resident in HBM
-before the timed region.  Batches are prepared by DistGNN.dataloading.PrefetchLoader with
---depth batches in flight (each on its own stream, over one sampler and one feature server;
-output identical to the sequential loop, which --depth 1 runs); the timed region holds exactly
-K batches.  N > 1 (torchrun): every rank holds the graph (replicated, weak
-scaling, independent replicas) and samples its own slice of the train nids; no collective
-runs in the timed loop.  --shard caches node v on GPU v mod N instead (remote rows read
-one-sided over xGMI through IPC-mapped peer memory).
+ops._CAPI_cuda_index_select(labels, seeds), on a synthetic products-like RMAT graph.  Inputs
+are resident in HBM before the timed region.  Batches are prepared by
+DistGNN.dataloading.PrefetchLoader with --depth batches in flight (each on its own stream, over
+one sampler and one feature server; output identical to the sequential loop, which --depth 1
+runs); the timed region holds exactly K batches per rank.
+
+Workloads (--mode):
+  replicated     configs[1] (the N = 1 default): whole graph + all features in every GPU's HBM.
+  feature-shard  configs[2] (the N > 1 default): the graph structure in every GPU's HBM, the
+                 feature rows sharded v mod N over the GPUs behind the P2P feature server
+                 (remote rows read one-sided over xGMI through IPC-mapped peer memory; setup
+                 collectives over RCCL).
+  shard          structure and features both sharded v mod N (neighbour lists read over xGMI
+                 too: the configs[4] "gather + xGMI p2p" stress layout).
+--cache-frac f < 1 keeps only the ceil(f*N) highest in-degree nodes in HBM (sharded by rank in
+the sharded modes); every other row is read zero-copy from pinned host memory.
+
+Launch: `python bench.py --gpus N` with no torchrun environment spawns N ranks itself (one
+process per GPU, before any GPU call); under torchrun (WORLD_SIZE set) WORLD_SIZE must equal
+--gpus.  With N > 1 local rank 0 builds the synthetic inputs once and every rank maps the same
+host copy from /dev/shm (the reference shares one host copy through mp.spawn,
+node_classification.py:325-328).  Every rank samples its own slice of the train nids; the timed
+loop has no collective.  value = sampled edges of all ranks / max-over-ranks time.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--scale S --ef E]
+                       [--mode replicated|feature-shard|shard] [--bias] [--cache-frac f]
 """
 import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,6 +48,12 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+XGMI_LINK_GBPS = 153.0  # one xGMI link per peer
+# the SURVEY 8(d) synthetic shapes by RMAT (scale, edge factor)
+WORKLOADS = {(17, 9): "arxiv-like", (21, 59): "products-like", (27, 12): "papers100M-like",
+             (26, 16): "RMAT-1B"}
+CONFIG_OF_MODE = {"replicated": "configs[1]", "feature-shard": "configs[2]",
+                  "shard": "configs[4] layout"}
 
 
 def log(*a):
@@ -38,7 +61,7 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=1000)
@@ -48,115 +71,168 @@ def parse():
     p.add_argument("--scale", type=int, default=21)   # products-like: 2,097,152 nodes
     p.add_argument("--ef", type=int, default=59)      # 123.7 M edges
     p.add_argument("--dim", type=int, default=100)
-    p.add_argument("--shard", action="store_true",
-                   help="cache node v on GPU v %% N (P2P over xGMI) instead of replicating")
+    p.add_argument("--mode", choices=["auto", "replicated", "feature-shard", "shard"],
+                   default="auto", help="auto = replicated at N = 1, feature-shard at N > 1")
+    p.add_argument("--shard", action="store_true", help="alias of --mode shard")
     p.add_argument("--bias", action="store_true",
                    help="biased (degree-weighted) sampler: probs[e] = 1 + indeg(indices[e])")
     p.add_argument("--cache-frac", type=float, default=1.0,
                    help="cache only the ceil(f*N) highest in-degree nodes in HBM; every other "
                         "row is read zero-copy from pinned host memory (SURVEY 8(f) rank 2)")
-    p.add_argument("--comm", choices=["gloo", "rccl"], default="gloo",
-                   help="transport of the library's setup collectives in --shard mode")
+    p.add_argument("--comm", choices=["auto", "gloo", "rccl"], default="auto",
+                   help="transport of the library's setup collectives at N > 1 (auto: RCCL, "
+                        "or the gloo host transport when ranks share a GPU)")
     p.add_argument("--depth", type=int, default=3,
                    help="batches in flight (PrefetchLoader streams); 1 = the sequential loop")
+    p.add_argument("--no-replicated-pass", action="store_true",
+                   help="N > 1: skip the secondary replicated measurement")
+    p.add_argument("--seq-calls", type=int, default=50,
+                   help="synchronous calls timed for sequential_value (SURVEY 8(d): >= 50)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--seed", type=int, default=20261015)
-    return p.parse_args()
+    a = p.parse_args(argv)
+    if a.shard:
+        a.mode = "shard"
+    return a
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # DGS_BENCH_SHARE_DEVICE=1 rehearses the N>1 flow on a 1-GPU box: every rank on cuda:0,
-    # gloo process group (RCCL refuses two ranks on one device).
-    share = os.environ.get("DGS_BENCH_SHARE_DEVICE") == "1"
-    if share:
-        local_rank = 0
-    torch.cuda.set_device(local_rank)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        if share:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    import dgs
-    from DistGNN.dataloading import PrefetchLoader, SeedGenerator
+def workload_name(scale, ef):
+    return WORKLOADS.get((scale, ef), f"RMAT scale {scale} ef {ef}")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` without a torchrun environment: run this script as N ranks (one process per
+    GPU) and return their exit status.  Nothing here touches the GPU before the ranks start
+    (counting devices does not initialise it on this image)."""
+    if os.environ.get("DGS_BENCH_SHARE_DEVICE") != "1" and torch.cuda.device_count() < n:
+        raise SystemExit(f"bench.py: --gpus {n} but only {torch.cuda.device_count()} GPUs are "
+                         "visible (DGS_BENCH_SHARE_DEVICE=1 rehearses N ranks on one GPU)")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
+
+
+def check_world(args, world_env):
+    """The rank count must be the one asked for: a mismatch would report a different
+    configuration than the caller named."""
+    world = int(world_env) if world_env is not None else 1
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch N ranks "
+                         "with --gpus N (torchrun --nproc-per-node N ... --gpus N)")
+    return world
+
+
+def resolve_mode(args, world):
+    if args.mode != "auto":
+        return args.mode
+    return "replicated" if world == 1 else "feature-shard"
+
+
+def cache_lists(mode, N, rank, world, hot):
+    """(sampler cache nids, feature cache nids) of this rank."""
+    def shard(all_ids):
+        return all_ids[rank::world] if world > 1 else all_ids
+    everything = hot if hot is not None else torch.arange(N)
+    if mode == "replicated" or world == 1:
+        return everything, everything
+    if mode == "feature-shard":
+        return everything, shard(everything)
+    return shard(everything), shard(everything)
+
+
+# ---------------------------------------------------------------------------- inputs
+def build_inputs(args, dev):
+    """The synthetic inputs on the host: CSC graph, optional degree-weighted probs, features,
+    labels (identical on every rank: fixed seeds)."""
     from DistGNN.dataloading.synthetic import rmat_csc_torch
-    if world > 1 and args.shard:
-        # setup collectives only (IPC handles, cache lists); the timed loop has none
-        if args.comm == "rccl" and not share:
-            from DistGNN.dist import create_communicator
-            create_communicator(world)
-        else:
-            dgs.ops._CAPI_set_host_comm(dist.group.WORLD if share
-                                        else dist.new_group(backend="gloo"))
-
-    fan_out = [int(x) for x in args.fan_out.split(",")]
-    dev = torch.device("cuda", local_rank)
-
-    # ---------------- synthetic inputs (identical on every rank)
-    t0 = time.time()
     indptr_d, indices_d = rmat_csc_torch(args.scale, args.ef, seed=args.seed, device=dev)
     N = indptr_d.numel() - 1
-    E = indices_d.numel()
     gen = torch.Generator(device=dev)
     gen.manual_seed(11)
     feats_d = torch.randn(N, args.dim, generator=gen, device=dev)
     labels_d = torch.randint(0, 47, (N,), generator=gen, device=dev)
-    probs = torch.Tensor()
-    hot = None
-    if args.cache_frac < 1.0:  # hot set: highest in-degree first (ties by id), kept on host
-        n_hot = max(1, int(math.ceil(args.cache_frac * N)))
-        indeg = torch.bincount(indices_d, minlength=indptr_d.numel() - 1)
-        hot = torch.sort(indeg, descending=True, stable=True).indices[:n_hot].cpu()
-        del indeg
+    out = {"indptr": indptr_d.cpu(), "indices": None, "probs": None}
     if args.bias:  # SURVEY 8(d): degree-weighted, probs[e] = float32(1 + indeg(indices[e]))
-        indeg = torch.bincount(indices_d, minlength=indptr_d.numel() - 1)
-        probs = (1 + indeg[indices_d]).to(torch.float32).cpu()
+        indeg = torch.bincount(indices_d, minlength=N)
+        out["probs"] = (1 + indeg[indices_d]).to(torch.float32).cpu()
         del indeg
-    indptr, indices = indptr_d.cpu(), indices_d.cpu()
-    feats, labels = feats_d.cpu(), labels_d.cpu()
+    out["indices"] = indices_d.cpu()
+    out["feats"] = feats_d.cpu()
+    out["labels"] = labels_d.cpu()
     del indptr_d, indices_d, feats_d, labels_d
     torch.cuda.empty_cache()
-    g2 = torch.Generator()
-    g2.manual_seed(2)
-    train = torch.randperm(N, generator=g2)[: N // 10]
-    train_local = seed_slice(train, rank, world).to(dev)
-    log(f"[bench] graph N={N} E={E} d={args.dim} built in {time.time() - t0:.1f}s")
+    return out
 
-    # ---------------- services: whole graph + all features in HBM (configs[1])
-    if hot is not None:
-        cache = hot[rank::world] if args.shard and world > 1 else hot
-    elif args.shard and world > 1:
-        cache = torch.arange(rank, N, world)
-    else:
-        cache = torch.arange(N)
-    # which nodes any GPU holds (the rest are host rows), for the host-row share reported below
-    cached_mask = torch.zeros(N, dtype=torch.bool, device=dev)
-    cached_mask[(hot if hot is not None else torch.arange(N)).to(dev)] = True
-    t0 = time.time()
-    sampler = dgs.classes.P2PCacheSampler(indptr, indices, probs, cache, local_rank)
-    server = dgs.classes.P2PCacheFeatureServer(feats, cache, local_rank)
-    labels_dev = labels.to(dev)
-    layout = server._layout()
-    torch.cuda.synchronize()
-    log(f"[bench] services ready in {time.time() - t0:.1f}s")
-    dgs.ops._CAPI_set_random_seed(args.seed + rank)
 
-    torch.manual_seed(1)
-    loader = iter(SeedGenerator(train_local, args.batch, shuffle=True, drop_last=True))
-
-    def next_seeds():
-        nonlocal loader
+def shared_inputs(args, dev, dist, local_rank, tag):
+    """N > 1: local rank 0 builds the inputs and writes them to /dev/shm; every rank maps the
+    same pages (one host copy per node, as the reference's mp.spawn shares one).  Falls back to
+    a copy per rank when /dev/shm cannot hold them (reported in the line)."""
+    names = ("indptr", "indices", "probs", "feats", "labels")
+    base = f"/dev/shm/dgs_bench_{tag}"
+    meta = [None]
+    if local_rank == 0:
+        inp = build_inputs(args, dev)
+        need = sum(t.numel() * t.element_size() for t in inp.values() if t is not None)
         try:
-            return next(loader)
-        except StopIteration:
-            loader = iter(SeedGenerator(train_local, args.batch, shuffle=True, drop_last=True))
-            return next(loader)
+            st = os.statvfs("/dev/shm")
+            room = st.f_bavail * st.f_frsize
+        except OSError:
+            room = 0
+        if room > need * 1.05 + (1 << 30):
+            m = {}
+            for k in names:
+                t = inp[k]
+                if t is None:
+                    continue
+                t.numpy().tofile(f"{base}_{k}")
+                m[k] = (list(t.shape), str(t.dtype).replace("torch.", ""))
+            meta = [m]
+        else:
+            meta = [{"_local": True}]
+    dist.broadcast_object_list(meta, 0)
+    m = meta[0]
+    if m.get("_local"):
+        inp = inp if local_rank == 0 else build_inputs(args, dev)
+        dist.barrier()
+        return inp, "per-rank copies (/dev/shm too small for one shared copy)"
+    out = {"probs": None}
+    for k, (shape, dt) in m.items():
+        n = int(np.prod(shape))
+        out[k] = torch.from_file(f"{base}_{k}", shared=True, size=n,
+                                 dtype=getattr(torch, dt)).view(*shape)
+    dist.barrier()  # every rank has mapped them: the names can go, the pages stay mapped
+    if local_rank == 0:
+        for k in m:
+            os.unlink(f"{base}_{k}")
+    return out, "one copy per node, mapped by every rank from /dev/shm"
+
+
+def hot_set(indices, N, frac, dev):
+    """The ceil(f*N) highest in-degree nodes (ties by id), or None for the whole graph."""
+    if frac >= 1.0:
+        return None
+    n_hot = max(1, int(math.ceil(frac * N)))
+    indeg = torch.bincount(indices.to(dev), minlength=N)
+    return torch.sort(indeg, descending=True, stable=True).indices[:n_hot].cpu()
+
+
+# ---------------------------------------------------------------------------- timed run
+def timed_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist, profile):
+    """W warm-up batches, then exactly K timed batches between barrier + synchronize on both
+    sides.  Returns (elapsed s, edges, rows, profile dict or None, host step gaps, mallocs)."""
+    from DistGNN.dataloading import PrefetchLoader
+    dev = labels_dev.device
 
     def step(seeds):
         """The sequential loop body.  The label gather depends only on the seeds: issued
@@ -184,7 +260,8 @@ def main():
     torch.cuda.synchronize()
     # only the gather kernel is measured in the timed region: its workgroups stamp their own
     # start / end (no stream markers between the measured kernels)
-    dgs.ops.profile_enable(dgs.ops.PROFILE_GATHER)
+    if profile:
+        dgs.ops.profile_enable(dgs.ops.PROFILE_GATHER)
     seg0 = torch.cuda.memory_stats(dev).get("segment.all.allocated", 0)
     edges = rows = 0
     t0 = time.perf_counter()
@@ -198,120 +275,228 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    prof = dgs.ops.profile_read()
+    prof = dgs.ops.profile_read() if profile else None
     # hipMalloc calls the caching allocator made inside the timed region (host stalls)
     mallocs = torch.cuda.memory_stats(dev).get("segment.all.allocated", 0) - seg0
     # host-side spacing of consecutive batches handed out by the loader (jitter diagnostics)
     gaps = np.diff(np.array([t0] + step_t)) * 1e3
     step_gaps = {"p10": float(np.percentile(gaps, 10)), "p50": float(np.median(gaps)),
                  "p90": float(np.percentile(gaps, 90)), "max": float(gaps.max())}
-    # informational, outside the timed region: the sequential loop's latency per sample call
-    # (host wall, sample + label select), its GPU span, and the feature gather on its own
-    n_side = min(args.steps, 20)
-    side_seeds = [next_seeds() for _ in range(n_side)]
-    torch.cuda.synchronize()
-    dgs.ops.profile_enable(dgs.ops.PROFILE_SAMPLE | dgs.ops.PROFILE_SELECT)
-    ts = time.perf_counter()
-    side_nids = []
-    for s in side_seeds:
-        dgs.ops._CAPI_cuda_index_select(labels_dev, s)
-        side_nids.append(sampler._CAPI_sample_node_classifiction(s, fan_out, False)[-1][1])
-    torch.cuda.synchronize()
-    seq_ms = (time.perf_counter() - ts) * 1e3 / n_side
-    side = dgs.ops.profile_read()
-    # share of the gathered rows that are host rows, over the side pass's batches (the timed
-    # loop keeps no batch alive: each one it held would pin its output buffers, and the
-    # caching allocator would hipMalloc fresh ones inside the timed region)
-    host_rows = sum(float((~cached_mask[n.long()]).sum()) / max(n.numel(), 1)
-                    for n in side_nids) / max(len(side_nids), 1)
-    dgs.ops.profile_enable(dgs.ops.PROFILE_GATHER)
-    iso_rows = 0
-    for n in side_nids:
-        iso_rows += server._CAPI_get_feature(n).shape[0]
-    torch.cuda.synchronize()
-    iso = dgs.ops.profile_read()
-    dgs.ops.profile_enable(False)
-    # SURVEY 8(d) metric (2) as defined there: algorithmic bytes / wall time of one synchronous
-    # _CAPI_get_feature call (host launch + kernel + synchronisation), median over the side pass
-    call_ms = []
-    for n in side_nids:
-        tc = time.perf_counter()
-        server._CAPI_get_feature(n)
-        torch.cuda.synchronize()
-        call_ms.append((time.perf_counter() - tc) * 1e3)
-    call_i = int(np.argsort(call_ms)[len(call_ms) // 2])
-    call_gbps = (side_nids[call_i].numel() * (2 * args.dim * 4 + 8) / (call_ms[call_i] * 1e-3) / 1e9
-                 if call_ms else 0.0)
+    return elapsed, edges, rows, prof, step_gaps, mallocs
 
+
+def reduce_over_ranks(dist, dev, elapsed, *work):
+    """Job time = max over ranks (every rank ran the same K steps between barriers); work =
+    sum over ranks.  dist is None for a single process."""
+    if dist is None:
+        return (elapsed,) + tuple(float(w) for w in work)
+    t = torch.tensor([elapsed] + [float(w) for w in work], dtype=torch.float64, device=dev)
+    mx = t.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return (float(mx[0]),) + tuple(float(x) for x in t[1:])
+
+
+def seed_slice(train, rank, world):
+    """Train nids of this rank (node_classification.py:312-321: contiguous equal slices)."""
+    per = (train.numel() + world - 1) // world
+    return train[rank * per:(rank + 1) * per]
+
+
+# ---------------------------------------------------------------------------- main
+def main():
+    args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = check_world(args, world_env)
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    mode = resolve_mode(args, world)
+    # DGS_BENCH_SHARE_DEVICE=1 rehearses the N > 1 flow on a 1-GPU box: every rank on cuda:0,
+    # gloo process group and host transport (RCCL refuses two ranks on one device).
+    share = os.environ.get("DGS_BENCH_SHARE_DEVICE") == "1"
+    dev_index = 0 if share else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    dist = None
+    comm = None
+    if world > 1:
+        import torch.distributed as dist
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    import dgs
+    from DistGNN.dataloading import SeedGenerator
+    if world > 1:
+        # the library's setup collectives (IPC handles, cache lists, barriers); none in the
+        # timed loop.  Every mode sets it up, so the secondary replicated pass is collective too.
+        comm = args.comm if args.comm != "auto" else ("gloo" if share else "rccl")
+        if comm == "rccl":
+            if share:
+                raise SystemExit("bench.py: RCCL refuses two ranks on one GPU; use --comm gloo")
+            from DistGNN.dist import create_communicator
+            create_communicator(world)
+        else:
+            dgs.ops._CAPI_set_host_comm(dist.group.WORLD if share
+                                        else dist.new_group(backend="gloo"))
+
+    fan_out = [int(x) for x in args.fan_out.split(",")]
+
+    # ---------------- synthetic inputs (identical on every rank)
+    t0 = time.time()
+    if world > 1:
+        port = os.environ.get("MASTER_PORT", "0")
+        inp, host_copy = shared_inputs(args, dev, dist, local_rank,
+                                       f"{port}_{os.environ.get('TORCHELASTIC_RUN_ID', '')}")
+    else:
+        inp, host_copy = build_inputs(args, dev), "single process"
+    indptr, indices, feats, labels = inp["indptr"], inp["indices"], inp["feats"], inp["labels"]
+    probs = inp["probs"] if args.bias else torch.Tensor()
+    N = indptr.numel() - 1
+    E = indices.numel()
+    hot = hot_set(indices, N, args.cache_frac, dev)
+    g2 = torch.Generator()
+    g2.manual_seed(2)
+    train = torch.randperm(N, generator=g2)[: N // 10]
+    train_local = seed_slice(train, rank, world).to(dev)
+    log(f"[bench] graph N={N} E={E} d={args.dim} built in {time.time() - t0:.1f}s "
+        f"({host_copy})")
+
+    # ---------------- services
+    s_cache, f_cache = cache_lists(mode, N, rank, world, hot)
+    # which nodes any GPU holds (the rest are host rows), for the host-row share reported below
+    cached_mask = torch.zeros(N, dtype=torch.bool, device=dev)
+    cached_mask[(hot if hot is not None else torch.arange(N)).to(dev)] = True
+    t0 = time.time()
+    sampler = dgs.classes.P2PCacheSampler(indptr, indices, probs, s_cache, dev_index)
+    server = dgs.classes.P2PCacheFeatureServer(feats, f_cache, dev_index)
+    labels_dev = labels.to(dev)
+    layout = server._layout()
+    torch.cuda.synchronize()
+    log(f"[bench] services ready in {time.time() - t0:.1f}s (mode {mode})")
+    dgs.ops._CAPI_set_random_seed(args.seed + rank)
+
+    torch.manual_seed(1)
+    loader = iter(SeedGenerator(train_local, args.batch, shuffle=True, drop_last=True))
+
+    def next_seeds():
+        nonlocal loader
+        try:
+            return next(loader)
+        except StopIteration:
+            loader = iter(SeedGenerator(train_local, args.batch, shuffle=True, drop_last=True))
+            return next(loader)
+
+    elapsed, edges, rows, prof, step_gaps, mallocs = timed_pass(
+        dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist, profile=True)
     row_bytes = args.dim * 4
-    gather_bytes = rows * (2 * row_bytes + 8)  # read row + write row + read nid
-    elapsed, edges_all, rows_all, gbytes_all = reduce_over_ranks(
-        dist, torch.device("cpu") if share else dev, elapsed, edges, rows, gather_bytes)
+    per_row = 2 * row_bytes + 8  # SURVEY 8(d): read row + write row + read nid
+    gather_bytes = rows * per_row
+    red_dev = torch.device("cpu") if share else dev
+    elapsed_all, edges_all, rows_all, gbytes_all = reduce_over_ranks(
+        dist, red_dev, elapsed, edges, rows, gather_bytes)
 
-    # roofline of the dominant HBM kernel (feature gather), measured live with HIP events
+    side = side_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, cached_mask,
+                     per_row)
+
+    # roofline of the dominant HBM kernel (feature gather), timed live by its own workgroups
     g_ms = prof["gather_ms"] / max(prof["gather_launches"], 1)
     g_bytes = gather_bytes / max(prof["gather_launches"], 1)
     achieved = g_bytes / (g_ms * 1e-3) / 1e9 if g_ms > 0 else 0.0
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "gather_pmc.json")
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get("dim") == args.dim:
-                traffic = pmc.get("hbm_bytes_per_row") * (rows / max(prof["gather_launches"], 1))
-        except Exception:
-            traffic = None
+    traffic, traffic_src = pmc_traffic(args.dim, rows / max(prof["gather_launches"], 1))
+
+    # ---------------- N > 1: the same K steps with everything replicated (secondary figure)
+    replicated = None
+    if world > 1 and mode != "replicated" and not args.no_replicated_pass:
+        del sampler, server  # collective destructors
+        torch.cuda.synchronize()
+        everything = hot if hot is not None else torch.arange(N)
+        sampler = dgs.classes.P2PCacheSampler(indptr, indices, probs, everything, dev_index)
+        server = dgs.classes.P2PCacheFeatureServer(feats, everything, dev_index)
+        dgs.ops._CAPI_set_random_seed(args.seed + rank)
+        r_el, r_ed, _, _, _, _ = timed_pass(dgs, sampler, server, labels_dev, fan_out, args,
+                                            next_seeds, dist, profile=False)
+        r_el, r_ed = reduce_over_ranks(dist, red_dev, r_el, r_ed)
+        replicated = {"value": r_ed / r_el, "unit": "sampled edges/s",
+                      "ms_per_step": r_el * 1e3 / args.steps,
+                      "workload": "whole graph + features in every GPU's HBM (configs[1] "
+                                  "layout on every rank)"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(indptr, indices, probs if args.bias else None, feats, train, fan_out,
-                           args)
+        cpu = cpu_baseline(indptr, indices, inp["probs"] if args.bias else None, feats, train,
+                           fan_out, args)
 
+    wl = workload_name(args.scale, args.ef)
+    sampler_kind = "biased (degree-weighted)" if args.bias else "uniform"
+    if mode == "replicated":
+        placement = ("whole graph + features in HBM" +
+                     (" on every GPU (independent replicas)" if world > 1 else ""))
+    elif mode == "feature-shard":
+        placement = (f"graph structure in every GPU's HBM, feature rows sharded v mod {world} "
+                     "over the GPUs (P2P feature server, remote rows over xGMI)")
+    else:
+        placement = (f"graph structure and feature rows sharded v mod {world} over the GPUs "
+                     "(remote neighbour lists and rows over xGMI)")
+    if hot is not None:
+        placement = (f"HBM cache of the {args.cache_frac:.0%} highest in-degree nodes "
+                     f"({'replicated' if mode == 'replicated' else 'sharded by rank'}), other "
+                     "rows zero-copy from pinned host")
     out = {
         "metric": "sampled edges/sec + feature-gather GB/s, fan-out [15,10,5]",
-        "value": edges_all / elapsed,
+        "value": edges_all / elapsed_all,
         "unit": "sampled edges/s",
+        "value_kind": (f"pipelined: DistGNN.dataloading.PrefetchLoader with {args.depth} batches "
+                       "in flight (additive API; --depth 1 = the reference loop); "
+                       "sequential_value = SURVEY 8(d)'s single synchronous "
+                       "_CAPI_sample_node_classifiction call" if args.depth > 1 else
+                       "sequential loop (the reference's three calls per batch)"),
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed * 1e3 / args.steps,
+        "ms_per_step": elapsed_all * 1e3 / args.steps,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (RMAT a,b,c,d=.57,.19,.19,.05; randn f32 features; no OGB offline)",
         "config": {
-            "workload": (f"products-like RMAT scale {args.scale} ef {args.ef} (N={N}, E={E}), "
-                         f"{'biased (degree-weighted)' if args.bias else 'uniform'} sampler "
-                         f"fan-out {fan_out} without replacement, B={args.batch} "
-                         f"seeds/step/GPU, + full-feature gather d={args.dim} f32 + label gather; "
-                         + (f"HBM cache of the {args.cache_frac:.0%} highest in-degree nodes "
-                            f"({'sharded' if args.shard and world > 1 else 'replicated'}), "
-                            "other rows zero-copy from pinned host" if hot is not None else
-                            "graph sharded v%N over GPUs (P2P)" if args.shard and world > 1
-                            else "whole graph + features in HBM on every GPU")),
+            "workload": (f"{wl} RMAT scale {args.scale} ef {args.ef} (N={N}, E={E}), "
+                         f"{sampler_kind} sampler fan-out {fan_out} without replacement, "
+                         f"B={args.batch} seeds/step/GPU, + feature gather d={args.dim} f32 + "
+                         f"label gather; {placement}"),
+            "baseline_config": CONFIG_OF_MODE[mode] if hot is None else "SURVEY 8(f) rank 2",
+            "mode": mode,
             "fan_out": fan_out, "batch_per_gpu": args.batch, "num_nodes": N, "num_edges": E,
             "feat_dim": args.dim, "parallelism": f"dp{world} (seed-parallel)",
             "cache_frac": args.cache_frac,
             "pipeline_depth": args.depth,
+            "setup_comm": comm,
+            "host_graph": host_copy,
         },
+        "sequential_value": side["sequential_value"],
+        "sequential_call_ms_median": side["seq_ms_median"],
+        "replicated": replicated,
         "host_step_gap_ms": step_gaps,
         "allocator_mallocs_in_timed_region": mallocs,
-        "host_row_share": host_rows,
+        "host_row_share": side["host_rows"],
         # host rows cross PCIe Gen5 x16 (63 GB/s spec): their read rate during the gather
-        "gather_host_read_GBps": (host_rows * rows * row_bytes / (prof["gather_ms"] * 1e-3) / 1e9
+        "gather_host_read_GBps": (side["host_rows"] * rows * row_bytes /
+                                  (prof["gather_ms"] * 1e-3) / 1e9
                                   if prof["gather_ms"] > 0 else 0.0),
         "gather_GBps": achieved,
-        "gather_GBps_wall": gbytes_all / elapsed / 1e9,
-        "gather_GBps_sync_call": call_gbps,
+        "gather_GBps_wall": gbytes_all / elapsed_all / 1e9,
+        "gather_GBps_sync_call": side["call_gbps"],
         "sampled_edges_per_step": edges_all / args.steps,
         "gathered_rows_per_step": rows_all / args.steps,
         "gather_kernel_ms_per_step": prof["gather_ms"] / args.steps,
-        "sample_span_ms_per_call": side["sample_ms"] / max(side["sample_calls"], 1),
-        "sequential_sample_ms_per_call": seq_ms,
-        "label_select_kernel_ms": side["select_ms"] / max(side["select_launches"], 1),
+        "sample_span_ms_per_call": side["sample_span_ms"],
+        "label_select_kernel_ms": side["select_ms"],
         "roofline": {
-            "bound": "hbm",
+            "bound": ("hbm" if world == 1 or mode == "replicated"
+                      else "hbm (local rows) + xGMI (remote rows)"),
             "kernel": ("k_gather<16, StridedSrc> (P2PCacheFeatureServer gather, computed row "
                        "addresses)" if layout >= 0 else
                        "k_gather<16, TableSrc> (P2PCacheFeatureServer gather, address table)"),
@@ -323,18 +508,22 @@ def main():
             "frac": achieved / HBM_PEAK_GBPS,
             "bytes_per_launch": g_bytes, "avg_launch_ms": g_ms,
             "traffic": traffic,
+            "traffic_source": traffic_src,
         },
         # the same gather kernel with nothing running beside it (sequential side pass)
         "roofline_isolated": {
-            "achieved": (iso_rows * (2 * args.dim * 4 + 8) / (iso["gather_ms"] * 1e-3) / 1e9
-                         if iso["gather_ms"] > 0 else 0.0),
-            "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": (iso_rows * (2 * args.dim * 4 + 8) / (iso["gather_ms"] * 1e-3) / 1e9
-                     / HBM_PEAK_GBPS if iso["gather_ms"] > 0 else 0.0),
-            "avg_launch_ms": iso["gather_ms"] / max(iso["gather_launches"], 1),
+            "achieved": side["iso_gbps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": side["iso_gbps"] / HBM_PEAK_GBPS,
+            "avg_launch_ms": side["iso_ms"],
         },
         "cpu_baseline": cpu,
     }
+    if world > 1 and mode != "replicated":
+        # (W-1)/W of a v mod W sharded gather's rows are remote, spread over W-1
+        # links of XGMI_LINK_GBPS, so row reads are bounded by W * XGMI_LINK_GBPS per GPU;
+        # the algorithmic bytes count each row twice (read + local write)
+        out["roofline"]["xgmi_bound_GBps"] = 2 * world * XGMI_LINK_GBPS
+        out["roofline"]["frac_of_xgmi_bound"] = achieved / (2 * world * XGMI_LINK_GBPS)
     if rank == 0:
         print(json.dumps(out), flush=True)
     del sampler, server  # collective destructors (sharded mode) before the group goes away
@@ -344,23 +533,83 @@ def main():
         dist.destroy_process_group()
 
 
-def reduce_over_ranks(dist, dev, elapsed, edges, rows, gather_bytes):
-    """Job time = max over ranks (every rank ran the same K steps between barriers); work =
-    sum over ranks.  dist is None for a single process."""
-    if dist is None:
-        return elapsed, float(edges), float(rows), float(gather_bytes)
-    t = torch.tensor([elapsed, float(edges), float(rows), float(gather_bytes)],
-                     dtype=torch.float64, device=dev)
-    mx = t.clone()
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(mx[0]), float(t[1]), float(t[2]), float(t[3])
+def pmc_traffic(dim, rows_per_launch):
+    """HBM bytes per gather launch from the committed PMC calibration of this row size
+    (rocprofv3 FETCH_SIZE / WRITE_SIZE passes, tools/pmc_traffic.py), or None when no
+    calibration exists for `dim`: counters cannot be read from inside this process."""
+    for name in (f"gather_pmc_d{dim}.json", "gather_pmc.json"):
+        path = os.path.join(ROOT, "profiles", name)
+        if not os.path.exists(path):
+            continue
+        try:
+            pmc = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if pmc.get("dim") == dim and pmc.get("hbm_bytes_per_row"):
+            return (pmc["hbm_bytes_per_row"] * rows_per_launch,
+                    f"profiles/{name} (rocprofv3 FETCH_SIZE/WRITE_SIZE per row at d={dim}) x "
+                    "this run's rows per launch")
+    return None, f"no PMC calibration committed for d={dim}"
 
 
-def seed_slice(train, rank, world):
-    """Train nids of this rank (node_classification.py:312-321: contiguous equal slices)."""
-    per = (train.numel() + world - 1) // world
-    return train[rank * per:(rank + 1) * per]
+def side_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, cached_mask,
+              per_row):
+    """Outside the timed region: SURVEY 8(d)'s synchronous per-call figures (median of
+    --seq-calls device-synchronised calls after 3 warm-ups), the sample call's GPU span, the
+    label select kernel, and the feature gather on its own."""
+    n_side = max(args.seq_calls, 3)
+    side_seeds = [next_seeds() for _ in range(n_side + 3)]
+    torch.cuda.synchronize()
+    for s in side_seeds[:3]:
+        sampler._CAPI_sample_node_classifiction(s, fan_out, False)
+    torch.cuda.synchronize()
+    side_nids, rates, call_ms = [], [], []
+    for s in side_seeds[3:]:
+        torch.cuda.synchronize()
+        tc = time.perf_counter()
+        blocks = sampler._CAPI_sample_node_classifiction(s, fan_out, False)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - tc
+        call_ms.append(dt * 1e3)
+        rates.append(sum(b[2].numel() for b in blocks) / dt)
+        side_nids.append(blocks[-1][1])
+    # GPU span of a sample call and the label select kernel (profiled, sequential)
+    dgs.ops.profile_enable(dgs.ops.PROFILE_SAMPLE | dgs.ops.PROFILE_SELECT)
+    for s in side_seeds[3:23]:
+        dgs.ops._CAPI_cuda_index_select(labels_dev, s)
+        sampler._CAPI_sample_node_classifiction(s, fan_out, False)
+    torch.cuda.synchronize()
+    sp = dgs.ops.profile_read()
+    # share of the gathered rows that are host rows
+    host_rows = sum(float((~cached_mask[n.long()]).sum()) / max(n.numel(), 1)
+                    for n in side_nids) / max(len(side_nids), 1)
+    dgs.ops.profile_enable(dgs.ops.PROFILE_GATHER)
+    iso_rows = 0
+    for n in side_nids:
+        iso_rows += server._CAPI_get_feature(n).shape[0]
+    torch.cuda.synchronize()
+    iso = dgs.ops.profile_read()
+    dgs.ops.profile_enable(False)
+    # SURVEY 8(d) metric (2): algorithmic bytes / wall time of one synchronous _CAPI_get_feature
+    # call (host launch + kernel + synchronisation), median over the side pass
+    g_rates = []
+    for n in side_nids:
+        torch.cuda.synchronize()
+        tc = time.perf_counter()
+        server._CAPI_get_feature(n)
+        torch.cuda.synchronize()
+        g_rates.append(n.numel() * per_row / (time.perf_counter() - tc) / 1e9)
+    return {
+        "sequential_value": float(np.median(rates)),
+        "seq_ms_median": float(np.median(call_ms)),
+        "sample_span_ms": sp["sample_ms"] / max(sp["sample_calls"], 1),
+        "select_ms": sp["select_ms"] / max(sp["select_launches"], 1),
+        "host_rows": host_rows,
+        "iso_gbps": (iso_rows * per_row / (iso["gather_ms"] * 1e-3) / 1e9
+                     if iso["gather_ms"] > 0 else 0.0),
+        "iso_ms": iso["gather_ms"] / max(iso["gather_launches"], 1),
+        "call_gbps": float(np.median(g_rates)) if g_rates else 0.0,
+    }
 
 
 def host_info():
@@ -377,7 +626,26 @@ def host_info():
         usable = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         usable = None
-    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "usable_cpus": usable}
+    quota = None
+    try:  # cgroup v2 CPU quota of this container, in CPUs
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "usable_cpus": usable,
+            "cgroup_cpu_quota": quota, "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def baseline_threads(info):
+    """The per-GPU share of the host: the container's CPU quota when one is set, else the
+    usable CPUs over the node's 8 GPUs (DGS_CPU_THREADS overrides).  Returns (threads, why)."""
+    if os.environ.get("DGS_CPU_THREADS"):
+        return int(os.environ["DGS_CPU_THREADS"]), "DGS_CPU_THREADS"
+    if info["cgroup_cpu_quota"]:
+        return max(1, int(info["cgroup_cpu_quota"])), "this container's cgroup CPU quota"
+    usable = info["usable_cpus"] or os.cpu_count() or 8
+    return max(1, usable // 8), "usable CPUs / 8 GPUs per node"
 
 
 def cpu_baseline(indptr, indices, probs, feats, train, fan_out, args):
@@ -385,13 +653,15 @@ def cpu_baseline(indptr, indices, probs, feats, train, fan_out, args):
     sampling per hop (uniform, or biased when probs is given) + relabel + feature gather, same
     graph and batch size."""
     from oracle import oracle as O
-    threads = int(os.environ.get("DGS_CPU_THREADS", "16"))
+    info = host_info()
+    threads, why = baseline_threads(info)
     ip, ix = indptr.numpy(), indices.numpy()
     pr = probs.numpy() if probs is not None else None
     fx = feats.numpy()
     rng = np.random.default_rng(1)
     seeds_all = train.numpy()
     edges = rows = batches = 0
+    t_gather = 0.0
     t0 = time.perf_counter()
     while True:
         seeds = seeds_all[rng.integers(0, seeds_all.size, args.batch)]
@@ -406,29 +676,35 @@ def cpu_baseline(indptr, indices, probs, feats, train, fan_out, args):
             uniq, (rr, cc) = O.relabel([cur, c], [r, c])
             edges += c.size
             cur = uniq
+        tg = time.perf_counter()
         x = O.index_select(fx, cur, nthreads=threads)
+        t_gather += time.perf_counter() - tg
         rows += x.shape[0]
         batches += 1
         if time.perf_counter() - t0 > args.cpu_baseline_seconds:
             break
     dt = time.perf_counter() - t0
+    per_row = 2 * args.dim * 4 + 8
     # the CPU gather baseline proper is torch.index_select on the host feature
-    # tensor with the same nids (here: the last batch's frontier, repeated for ~1 s)
+    # tensor.  Cache-cold: a fresh random id set of the frontier's size for every repeat, over
+    # all N rows (the feature matrix is far larger than the last-level cache).
     torch.set_num_threads(threads)
-    nid = torch.from_numpy(np.ascontiguousarray(cur))
+    n_ids = int(cur.size)
+    g = torch.Generator().manual_seed(5)
+    id_sets = [torch.randint(0, feats.shape[0], (n_ids,), generator=g) for _ in range(16)]
     reps, t1 = 0, time.perf_counter()
     while reps < 3 or time.perf_counter() - t1 < 1.0:
-        torch.index_select(feats, 0, nid)
+        torch.index_select(feats, 0, id_sets[reps % len(id_sets)])
         reps += 1
-    ts_gbps = reps * nid.numel() * (2 * args.dim * 4 + 8) / (time.perf_counter() - t1) / 1e9
-    return {"value": edges / dt, "unit": "sampled edges/s", "cores": threads, "kind": "port",
-            "host": host_info(),
-            "gather_GBps": rows * (2 * args.dim * 4 + 8) / dt / 1e9,
-            "gather_GBps_torch_index_select": ts_gbps,
+    ts_gbps = reps * n_ids * per_row / (time.perf_counter() - t1) / 1e9
+    return {"value": edges / dt, "unit": "sampled edges/s", "cores": threads,
+            "cores_basis": why, "kind": "port", "host": info,
+            "gather_GBps": rows * per_row / t_gather / 1e9 if t_gather > 0 else 0.0,
+            "gather_GBps_torch_index_select_cold": ts_gbps,
             "sample": (f"{batches} batches of B={args.batch}, fan-out {fan_out}, same graph; "
                        f"oracle/dgs_oracle.c OpenMP {'biased' if probs is not None else 'uniform'} "
-                       f"sampler ({threads} threads) + serial relabel "
-                       f"+ OpenMP gather, {dt:.1f}s")}
+                       f"sampler ({threads} threads) + serial relabel + OpenMP gather, {dt:.1f}s "
+                       f"(gather_GBps: the gather's own time, {t_gather:.2f}s)")}
 
 
 if __name__ == "__main__":

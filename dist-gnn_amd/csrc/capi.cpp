@@ -7,6 +7,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "services.h"
@@ -51,28 +52,66 @@ T *dev_ptr(T *p, const char *what) {
   return p;
 }
 
+// Device-memory check for the per-batch entry points, remembered per address: a caching
+// allocator hands the same few blocks back batch after batch, so the pointer query runs about
+// once per block (a host pointer fails here instead of faulting on the GPU later).
+void check_device_cached(const void *p, const char *what) {
+  thread_local std::unordered_set<uintptr_t> seen;
+  if (!p) throw Error(std::string(what) + " is null");
+  if (seen.count((uintptr_t)p)) return;
+  if (!is_device_pointer(p)) throw Error(std::string(what) + " must be device memory");
+  if (seen.size() >= 4096) seen.clear();
+  seen.insert((uintptr_t)p);
+}
+
 // Scratch of the standalone ops (dgs_sample_neighbors, dgs_relabel), one per (device, stream):
 // calls on different streams or threads never share buffers, calls on one stream are ordered
 // by the stream, and the returned lock serialises the host side of calls on one stream.  (The
-// reference allocates per call through the caching allocator.)
+// reference allocates per call through the caching allocator.)  At most kOpScratchMax entries
+// are kept: a caller cycling through short-lived streams evicts the least recently used idle
+// entry (its buffers are freed after a device synchronisation, so no launch still uses them).
 struct OpScratch {
   std::mutex mu;
   HopScratch ws;
+  uint64_t last_use = 0;
 };
-std::unique_lock<std::mutex> op_scratch(hipStream_t st, HopScratch **ws) {
+struct OpScratchLease {
+  std::shared_ptr<OpScratch> o;  // keeps an entry evicted meanwhile alive until the call ends
+  std::unique_lock<std::mutex> lk;
+};
+constexpr size_t kOpScratchMax = 16;
+OpScratchLease op_scratch(hipStream_t st, HopScratch **ws) {
   static std::mutex m;
-  static std::map<std::pair<int, hipStream_t>, std::unique_ptr<OpScratch>> all;
+  static std::map<std::pair<int, hipStream_t>, std::shared_ptr<OpScratch>> all;
+  static uint64_t tick = 0;
   int dev = 0;
   DGS_HIP(hipGetDevice(&dev));
-  OpScratch *o;
+  std::shared_ptr<OpScratch> o, evicted;
   {
     std::lock_guard<std::mutex> g(m);
-    std::unique_ptr<OpScratch> &p = all[{dev, st}];
-    if (!p) p.reset(new OpScratch);
-    o = p.get();
+    std::shared_ptr<OpScratch> &p = all[{dev, st}];
+    if (!p) p = std::make_shared<OpScratch>();
+    p->last_use = ++tick;
+    o = p;
+    if (all.size() > kOpScratchMax) {
+      auto victim = all.end();
+      for (auto it = all.begin(); it != all.end(); ++it)
+        if (it->second != o && it->second.use_count() == 1 &&
+            (victim == all.end() || it->second->last_use < victim->second->last_use))
+          victim = it;
+      if (victim != all.end()) {
+        evicted = std::move(victim->second);
+        all.erase(victim);
+      }
+    }
+  }
+  if (evicted) {
+    (void)hipDeviceSynchronize();  // its stream may be gone: wait for everything instead
+    evicted.reset();
   }
   *ws = &o->ws;
-  return std::unique_lock<std::mutex>(o->mu);
+  OpScratchLease lease{o, std::unique_lock<std::mutex>(o->mu)};
+  return lease;
 }
 // `consumer` waits (on the device) for the work enqueued on `producer` so far.  One event per
 // calling thread and device: a wait already enqueued keeps the record it saw, so the event can
@@ -168,16 +207,14 @@ int dgs_host_register(void *ptr, int64_t bytes) {
   return guard([&] {
     if (!ptr || bytes <= 0) return;
     // through the library's refcounted registry, shared with the services' host views
-    bool ref = false;
-    (void)device_view(ptr, bytes, &ref);
-    DGS_CHECK(ref, "host_register: the memory is already pinned outside this library");
+    host_pin(ptr, bytes);
   });
 }
 
 int dgs_host_unregister(void *ptr) {
   return guard([&] {
     if (!ptr) return;
-    release_host_view(ptr);
+    host_unpin(ptr);
   });
 }
 
@@ -210,7 +247,9 @@ int dgs_loader_gather(dgs_sampler *s, dgs_feature_server *fs, void *producer, vo
       stream_wait_impl(producer, consumer);
     const bool want_labels = labels && n_seeds > 0;
     // 4- and 8-byte label rows ride in the feature gather's launch
-    const bool fuse = want_labels && fs && n > 0 && n_seeds < (int64_t(1) << 31) &&
+    // (a zero-width feature matrix launches no gather: its labels go on their own)
+    const bool fuse = want_labels && fs && n > 0 && fs->s->row_bytes() > 0 &&
+                      n_seeds < (int64_t(1) << 31) &&
                       (label_row_bytes == 4 || label_row_bytes == 8) &&
                       ((uintptr_t)labels % label_row_bytes) == 0 &&
                       ((uintptr_t)label_out % label_row_bytes) == 0;
@@ -243,7 +282,7 @@ int dgs_sample_neighbors(const int64_t *seeds, int64_t Sn, const int64_t *indptr
     src.num_nodes = INT64_MAX;  // no node count at this boundary (reference: unchecked)
     seeds = dev_ptr(seeds, "seeds");
     HopScratch *wsp = nullptr;
-    const std::unique_lock<std::mutex> lk = op_scratch(st, &wsp);
+    const OpScratchLease lk = op_scratch(st, &wsp);
     HopScratch &ws = *wsp;
     int64_t *tmp = nullptr;  // [0] = nnz, then rowpos[S*k]
     const int64_t cap = Sn * num_picks;
@@ -285,7 +324,7 @@ int dgs_relabel(const int64_t *const *maps, const int64_t *map_sizes, int n_maps
     }
     int64_t *d_cnt = buf + nm + 2 * nr;
     HopScratch *ws = nullptr;
-    const std::unique_lock<std::mutex> lk = op_scratch(st, &ws);
+    const OpScratchLease lk = op_scratch(st, &ws);
     relabel_generic(buf, nm, buf + nm, nr, unique_out, buf + nm + nr, d_cnt, *ws, st);
     off = nm + nr;
     for (int i = 0; i < n_reqs; ++i) {
@@ -422,6 +461,8 @@ int dgs_sampler_sample_begin_after(dgs_sampler *s, void *wait_for, const int64_t
   return guard([&] {
     DGS_CHECK((flags & ~DGS_SAMPLE_HOST_ASYNC) == 0, "sample_begin: unknown flags");
     DGS_CHECK(L > 0 && L <= 64, "sample_begin: 1 to 64 hops");
+    if (n_seeds > 0) check_device_cached(seeds, "seeds");
+    check_device_cached(out, "out");
     int64_t fcap[64], ecap[64];
     int64_t *fr[64], *rows[64], *cols[64];
     s->s->bounds(n_seeds, fan_out, L, fcap, ecap);

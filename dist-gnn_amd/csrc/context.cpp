@@ -162,10 +162,21 @@ std::map<uintptr_t, HostReg>::iterator host_reg_find(const void *p) {
   --it;
   return x < it->first + it->second.bytes ? it : m.end();
 }
-}  // namespace
-
-void release_host_view(const void *p) {
-  std::lock_guard<std::mutex> g(host_reg_mu());
+// whether a registered range intersects [p, p + n) (caller holds the lock)
+bool host_reg_overlaps(uintptr_t p, size_t n) {
+  auto &m = host_regs();
+  auto it = m.lower_bound(p + n);  // first range starting at or after the end
+  if (it == m.begin()) return false;
+  --it;                             // the last range starting before the end
+  return it->first + it->second.bytes > p;
+}
+// Pins taken through dgs_host_register, by the pointer the caller passed: an unregister must
+// name one of them (it cannot drop a reference a service holds).
+std::map<uintptr_t, int> &abi_pins() {
+  static std::map<uintptr_t, int> m;
+  return m;
+}
+void release_locked(const void *p) {
   auto it = host_reg_find(p);
   if (it == host_regs().end()) return;
   if (--it->second.refs == 0) {
@@ -173,15 +184,39 @@ void release_host_view(const void *p) {
     host_regs().erase(it);
   }
 }
+}  // namespace
+
+void release_host_view(const void *p) {
+  std::lock_guard<std::mutex> g(host_reg_mu());
+  release_locked(p);
+}
+
+void host_pin(void *p, int64_t bytes) {
+  bool ref = false;
+  (void)device_view(p, bytes, &ref);
+  DGS_CHECK(ref, "host_register: the memory is already pinned outside this library");
+  std::lock_guard<std::mutex> g(host_reg_mu());
+  ++abi_pins()[(uintptr_t)p];
+}
+
+void host_unpin(void *p) {
+  std::lock_guard<std::mutex> g(host_reg_mu());
+  auto it = abi_pins().find((uintptr_t)p);
+  DGS_CHECK(it != abi_pins().end(),
+            "host_unregister: this pointer holds no dgs_host_register pin (pass the pointer "
+            "that was registered)");
+  if (--it->second == 0) abi_pins().erase(it);
+  release_locked(p);
+}
 
 void *device_view(const void *p, int64_t bytes, bool *registered_here) {
   if (registered_here) *registered_here = false;
   if (!p) return nullptr;
+  const size_t nb = (size_t)(bytes > 0 ? bytes : 1);
   std::lock_guard<std::mutex> g(host_reg_mu());
   {
     auto it = host_reg_find(p);
-    if (it != host_regs().end() && (uintptr_t)p + (size_t)(bytes > 0 ? bytes : 1) <=
-                                       it->first + it->second.bytes) {
+    if (it != host_regs().end() && (uintptr_t)p + nb <= it->first + it->second.bytes) {
       // a range registered here already: share it
       void *d = nullptr;
       DGS_HIP(hipHostGetDevicePointer(&d, reinterpret_cast<void *>(it->first), 0));
@@ -189,6 +224,12 @@ void *device_view(const void *p, int64_t bytes, bool *registered_here) {
       if (registered_here) *registered_here = true;
       return static_cast<char *>(d) + ((uintptr_t)p - it->first);
     }
+    // A range that only partly lies in one of this library's registrations cannot be mapped:
+    // a second registration over the same pages is refused by HIP, and the pointer query below
+    // would return a view of the registered part only, with no reference held on it.
+    DGS_CHECK(!host_reg_overlaps((uintptr_t)p, nb),
+              "host range overlaps a registration made for a different range of the same "
+              "buffer; register (pin) the whole buffer first");
   }
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) == hipSuccess) {
@@ -205,7 +246,6 @@ void *device_view(const void *p, int64_t bytes, bool *registered_here) {
     (void)hipGetLastError();
   }
   // pageable host memory: register it (mapped) for zero-copy device reads
-  const size_t nb = (size_t)(bytes > 0 ? bytes : 1);
   DGS_HIP(hipHostRegister(const_cast<void *>(p), nb, hipHostRegisterMapped));
   void *d = nullptr;
   const hipError_t e = hipHostGetDevicePointer(&d, const_cast<void *>(p), 0);

@@ -83,8 +83,13 @@ class Comm {
 // *registered_here is set so the owner can unregister it.
 // *registered_here = true: the view holds a reference on a registration made by this library
 // (shared by every view into the range); release it with release_host_view(p).
+// A range that partly overlaps one of this library's registrations is refused (Error).
 void *device_view(const void *p, int64_t bytes, bool *registered_here);
 void release_host_view(const void *p);
+// dgs_host_register / dgs_host_unregister: a reference on the registration plus a pin keyed by
+// `p`; unpinning a pointer that holds no pin is an error.
+void host_pin(void *p, int64_t bytes);
+void host_unpin(void *p);
 bool is_device_pointer(const void *p);
 
 }  // namespace dgs

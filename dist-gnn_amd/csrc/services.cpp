@@ -173,6 +173,7 @@ Sampler::~Sampler() {
       {
         std::lock_guard<std::mutex> g(c.mu);
         c.stop = true;
+        c.stop_flag.store(true, std::memory_order_relaxed);
       }
       c.cv.notify_all();
       c.launcher.join();
@@ -293,20 +294,29 @@ void Sampler::launcher_loop(Ctx &c, int dev) {
     const char *e = std::getenv("DGS_LAUNCHER_SPIN_US");
     return (e ? (int64_t)std::atoll(e) : (int64_t)1000) * 1000;
   }();
+  // Adaptive: the thread spins only while jobs keep arriving within the window (a loader's
+  // batch cadence); once a wait outlasts it, the next waits sleep until a job again comes
+  // within the window of the previous one, so an idle sampler holds no core.
+  bool spin = spin_ns > 0;
+  auto idle_since = std::chrono::steady_clock::now();
   std::unique_lock<std::mutex> lk(c.mu);
   for (;;) {
-    if (spin_ns > 0 && !c.job_ready && !c.stop) {
+    if (spin && !c.job_ready && !c.stop) {
       lk.unlock();
-      const auto t0 = std::chrono::steady_clock::now();
       for (uint32_t i = 1; !c.job_flag.load(std::memory_order_acquire); ++i) {
         __builtin_ia32_pause();
-        if ((i & 63) == 0 && std::chrono::duration_cast<std::chrono::nanoseconds>(
-                                 std::chrono::steady_clock::now() - t0).count() > spin_ns)
+        if ((i & 63) == 0 &&
+            (c.stop_flag.load(std::memory_order_relaxed) ||
+             std::chrono::duration_cast<std::chrono::nanoseconds>(
+                 std::chrono::steady_clock::now() - idle_since).count() > spin_ns))
           break;
       }
       lk.lock();
     }
     c.cv.wait(lk, [&] { return c.job_ready || c.stop; });
+    if (spin_ns > 0)
+      spin = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                 std::chrono::steady_clock::now() - idle_since).count() <= spin_ns;
     if (c.stop) return;
     c.job_ready = false;
     c.job_flag.store(false, std::memory_order_relaxed);
@@ -322,6 +332,7 @@ void Sampler::launcher_loop(Ctx &c, int dev) {
     c.job_err = err;
     c.job_done = true;
     c.cv.notify_all();
+    idle_since = std::chrono::steady_clock::now();
   }
 }
 

@@ -120,6 +120,7 @@ class Sampler {
     Job job;
     bool job_ready = false, job_done = true, stop = false;
     std::atomic<bool> job_flag{false};  // job_ready, readable without the lock (launcher spin)
+    std::atomic<bool> stop_flag{false};  // stop, likewise
     std::exception_ptr job_err;
     HopScratch ws;
     DevBuf dpair[2];  // direct relabel tables over node ids ((first position, label) pairs),
@@ -152,6 +153,7 @@ class FeatureServer {
   const void *local() const { return feat_srv_ ? feat_srv_->local() : nullptr; }
   int64_t local_rows() const { return feat_srv_ ? feat_srv_->items(rank_) : 0; }
   int layout() const { return wshift_; }
+  int64_t row_bytes() const { return row_bytes_; }
 
  private:
   int64_t num_rows_ = 0, row_bytes_ = 0;

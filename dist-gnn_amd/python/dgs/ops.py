@@ -21,9 +21,10 @@ __all__ = [
     "_CAPI_set_random_seed", "_CAPI_set_host_comm", "draw_launch_seeds",
 ]
 
-# host storage registered by _CAPI_tensor_pin_memory: data_ptr -> the tensor.  Holding the
-# tensor keeps its memory alive while registered (a registration outliving its allocation
-# would make HIP reject later copies through memory the allocator reuses).
+# host storage registered by _CAPI_tensor_pin_memory: data_ptr -> (the tensor, the registered
+# storage base).  Holding the tensor keeps its memory alive while registered (a registration
+# outliving its allocation would make HIP reject later copies through memory the allocator
+# reuses).
 _registered = {}
 
 
@@ -127,12 +128,17 @@ def _Test_NCCLTensorAllGather(local_tensor):
 
 # ------------------------------------------------------------------ pinning
 def _CAPI_tensor_pin_memory(data):
-    """pin_memory.cc:7-12 -- register the tensor's host storage (mapped) in place."""
+    """pin_memory.cc:7-12 -- register the tensor's host storage (mapped) in place.  The whole
+    storage is registered (the reference registers the tensor's own range): any view of the
+    buffer, including a later service's, then maps through this one registration."""
     if data.is_cuda or data.is_pinned() or data.numel() == 0:
         return
     p = data.data_ptr()
-    check(lib.dgs_host_register(ctypes.c_void_p(p), data.numel() * data.element_size()))
-    _registered[p] = data
+    if p in _registered:
+        return
+    st = data.untyped_storage()
+    check(lib.dgs_host_register(ctypes.c_void_p(st.data_ptr()), st.nbytes()))
+    _registered[p] = (data, st.data_ptr())
 
 
 def _CAPI_tensor_unpin_memory(data):
@@ -142,7 +148,7 @@ def _CAPI_tensor_unpin_memory(data):
         return
     p = data.data_ptr()
     if p in _registered:
-        check(lib.dgs_host_unregister(ctypes.c_void_p(p)))
+        check(lib.dgs_host_unregister(ctypes.c_void_p(_registered[p][1])))
         del _registered[p]
 
 

@@ -1,0 +1,104 @@
+"""Host logic of bench.py (no GPU): rank-count checks, workload placement per mode, and the
+one-host-copy input sharing of N > 1 runs (gloo world 2 on CPU)."""
+import glob
+import os
+import socket
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_world_mismatch_fails_loudly():
+    args = bench.parse(["--gpus", "4"])
+    with pytest.raises(SystemExit, match="WORLD_SIZE=2 but --gpus 4"):
+        bench.check_world(args, "2")
+    with pytest.raises(SystemExit, match="WORLD_SIZE=1 but --gpus 4"):
+        bench.check_world(args, None)
+    assert bench.check_world(bench.parse(["--gpus", "2"]), "2") == 2
+    assert bench.check_world(bench.parse([]), None) == 1
+
+
+def test_spawn_refuses_more_ranks_than_gpus(monkeypatch):
+    monkeypatch.delenv("DGS_BENCH_SHARE_DEVICE", raising=False)
+    with pytest.raises(SystemExit, match="GPUs are visible"):
+        bench.launch_ranks(max(torch.cuda.device_count(), 1) + 1, [])
+
+
+def test_modes_and_cache_lists():
+    assert bench.resolve_mode(bench.parse([]), 1) == "replicated"
+    assert bench.resolve_mode(bench.parse(["--gpus", "8"]), 8) == "feature-shard"
+    assert bench.parse(["--shard"]).mode == "shard"
+    N, W = 37, 4
+    allv = torch.arange(N)
+    for r in range(W):
+        s, f = bench.cache_lists("replicated", N, r, W, None)
+        assert torch.equal(s, allv) and torch.equal(f, allv)
+        s, f = bench.cache_lists("feature-shard", N, r, W, None)
+        assert torch.equal(s, allv) and torch.equal(f, torch.arange(r, N, W))
+        s, f = bench.cache_lists("shard", N, r, W, None)
+        assert torch.equal(s, torch.arange(r, N, W)) and torch.equal(f, s)
+    hot = torch.tensor([5, 1, 9, 3, 7])
+    s, f = bench.cache_lists("feature-shard", N, 1, 2, hot)
+    assert torch.equal(s, hot) and torch.equal(f, torch.tensor([1, 3]))
+    # the union of the sharded feature lists is every node exactly once
+    parts = torch.cat([bench.cache_lists("feature-shard", N, r, W, None)[1] for r in range(W)])
+    assert torch.equal(torch.sort(parts).values, allv)
+
+
+def test_workload_names():
+    assert bench.workload_name(21, 59) == "products-like"
+    assert bench.workload_name(27, 12) == "papers100M-like"
+    assert bench.workload_name(26, 16) == "RMAT-1B"
+    assert bench.workload_name(17, 9) == "arxiv-like"
+    assert bench.workload_name(12, 3) == "RMAT scale 12 ef 3"
+
+
+def test_baseline_threads_rule(monkeypatch):
+    monkeypatch.delenv("DGS_CPU_THREADS", raising=False)
+    info = {"cgroup_cpu_quota": None, "usable_cpus": 256}
+    assert bench.baseline_threads(info) == (32, "usable CPUs / 8 GPUs per node")
+    info["cgroup_cpu_quota"] = 16.0
+    assert bench.baseline_threads(info)[0] == 16
+    monkeypatch.setenv("DGS_CPU_THREADS", "3")
+    assert bench.baseline_threads(info) == (3, "DGS_CPU_THREADS")
+
+
+def _shared_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    args = bench.parse(["--gpus", str(world), "--scale", "8", "--ef", "4", "--dim", "6",
+                        "--bias"])
+    inp, how = bench.shared_inputs(args, torch.device("cpu"), dist, rank, f"test{port}")
+    torch.save({k: (v.clone() if v is not None else None) for k, v in inp.items()} | {"how": how},
+               f"{out}/r{rank}.pt")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shared_inputs_one_host_copy(tmp_path):
+    """Local rank 0 builds the inputs once; both ranks map the same /dev/shm pages and see
+    identical tensors; the file names are gone once every rank has mapped them."""
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_shared_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
+    assert r0["how"].startswith("one copy per node")
+    for k in ("indptr", "indices", "probs", "feats", "labels"):
+        assert torch.equal(r0[k], r1[k]), k
+    n = 1 << 8
+    assert r0["indptr"].numel() == n + 1 and r0["indices"].numel() == n * 4
+    assert r0["feats"].shape == (n, 6)
+    deg = torch.bincount(r0["indices"], minlength=n)
+    assert torch.equal(r0["probs"], (1 + deg[r0["indices"]]).float())
+    assert not glob.glob(f"/dev/shm/dgs_bench_test{port}_*")

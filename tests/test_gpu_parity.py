@@ -408,7 +408,7 @@ def test_pinned_tensor_outlives_caller_reference(dgs):
     for _ in range(8):  # host allocations + device round trips that could reuse the range
         h = torch.randn(1 << 16)
         assert torch.equal(h.cuda().cpu(), h)
-    kept = dgs.ops._registered[p]
+    kept = dgs.ops._registered[p][0]
     assert kept.data_ptr() == p and int(kept[-1]) == (1 << 16) - 1
     dgs.ops._CAPI_tensor_unpin_memory(kept)
     assert p not in dgs.ops._registered
@@ -502,3 +502,63 @@ def test_unpin_keeps_a_live_service_mapped(dgs):
     q = rng.integers(0, 1500, 2048)
     assert np.array_equal(fs._CAPI_get_feature(_cuda(q)).cpu().numpy(),
                           O.index_select(data.numpy(), q))
+
+
+def test_overlapping_views_share_one_registration(dgs):
+    """Services over different views of one pageable buffer (data[:k], then data) map the
+    buffer's single registration: destroying the first leaves the second's rows mapped and
+    byte-exact (the binding registers whole storages, pin_memory.cc:7-19)."""
+    import gc
+    rng = np.random.default_rng(8)
+    data = torch.from_numpy(rng.standard_normal((3000, 48)).astype(np.float32))
+    k = 1000
+    a = dgs.classes.P2PCacheFeatureServer(data[:k], torch.tensor([2]), 0)
+    b = dgs.classes.P2PCacheFeatureServer(data, torch.tensor([7]), 0)
+    c = dgs.classes.P2PCacheFeatureServer(data[k:], torch.tensor([0]), 0)
+    qa, qb = rng.integers(0, k, 2048), rng.integers(0, 3000, 4096)
+    assert np.array_equal(a._CAPI_get_feature(_cuda(qa)).cpu().numpy(),
+                          O.index_select(data[:k].numpy(), qa))
+    del a
+    gc.collect()
+    torch.cuda.synchronize()
+    assert np.array_equal(b._CAPI_get_feature(_cuda(qb)).cpu().numpy(),
+                          O.index_select(data.numpy(), qb))
+    qc = rng.integers(0, 3000 - k, 2048)
+    assert np.array_equal(c._CAPI_get_feature(_cuda(qc)).cpu().numpy(),
+                          O.index_select(data[k:].numpy(), qc))
+
+
+def test_c_abi_registration_rules(dgs):
+    """At the C ABI: a range that only partly lies in a registration the library made is
+    refused (no unreferenced, partly unmapped view), an unregister must name a pointer that
+    dgs_host_register pinned, and a contained range shares the registration."""
+    import ctypes
+    from dgs._lib import lib
+    buf = torch.zeros(1 << 16, dtype=torch.uint8)
+    base = buf.data_ptr()
+    assert lib.dgs_host_register(ctypes.c_void_p(base), 4096) == 0
+    # starts inside the registration, ends past it
+    assert lib.dgs_host_register(ctypes.c_void_p(base + 1024), 8192) != 0
+    assert b"overlaps" in lib.dgs_last_error()
+    # a service over such a range is refused the same way
+    with pytest.raises(RuntimeError, match="overlaps"):
+        _raw_feature_server(base + 1024, 256, 32)
+    # contained: shares, and needs its own unregister
+    assert lib.dgs_host_register(ctypes.c_void_p(base + 512), 1024) == 0
+    assert lib.dgs_host_unregister(ctypes.c_void_p(base + 7)) != 0  # never pinned
+    assert lib.dgs_host_unregister(ctypes.c_void_p(base + 512)) == 0
+    assert lib.dgs_host_unregister(ctypes.c_void_p(base + 512)) != 0  # already released
+    assert lib.dgs_host_unregister(ctypes.c_void_p(base)) == 0
+    # everything released: the larger range registers cleanly now
+    assert lib.dgs_host_register(ctypes.c_void_p(base + 1024), 8192) == 0
+    assert lib.dgs_host_unregister(ctypes.c_void_p(base + 1024)) == 0
+
+
+def _raw_feature_server(ptr, rows, row_bytes):
+    import ctypes
+    from dgs._lib import check, lib
+    h = ctypes.c_void_p()
+    nids = torch.tensor([0], dtype=torch.int64)
+    check(lib.dgs_feature_server_create(ctypes.c_void_p(ptr), rows, row_bytes,
+                                        ctypes.c_void_p(nids.data_ptr()), 1, 0, ctypes.byref(h)))
+    lib.dgs_feature_server_destroy(h)

@@ -281,17 +281,22 @@ def test_loader_streams_are_returned(dgs):
     assert len(P._FREE_STREAMS[dev]) >= 4
 
 
-@pytest.mark.parametrize("kind", ["int64", "int32", "float32", "int64x3", "no_server"])
+@pytest.mark.parametrize("kind", ["int64", "int32", "float32", "int64x3", "no_server",
+                                  "zero_width"])
 def test_prefetch_label_rows(dgs, kind):
     """The label gather rides in the feature gather's launch for 4- and 8-byte label rows
-    (dgs_loader_gather); wider rows and server-less loaders take the separate gather."""
+    (dgs_loader_gather); wider rows, server-less loaders and zero-width feature matrices (no
+    feature launch to ride in) take the separate gather."""
     from DistGNN.dataloading import PrefetchLoader
     _, sampler, server, labels, feats = _services(dgs, False)
     base = labels.long()
     lab = {"int64": base, "int32": base.int(), "float32": base.float() * 0.5 + 0.25,
            "int64x3": torch.stack([base, base * 3, -base], 1),
-           "no_server": base}[kind]
+           "no_server": base, "zero_width": base}[kind]
     srv = None if kind == "no_server" else server
+    if kind == "zero_width":
+        feats = torch.empty((feats.shape[0], 0), dtype=torch.float32)
+        srv = dgs.classes.P2PCacheFeatureServer(feats, torch.arange(1, feats.shape[0], 2), 0)
     batches = _batches(base.numel(), nb=6)
     got = list(PrefetchLoader(sampler, batches, [5, 3], server=srv, labels=lab, depth=3))
     torch.cuda.synchronize()
