@@ -12,10 +12,13 @@ runs); the timed region holds exactly K batches per rank.
 
 Workloads (--mode):
   replicated     configs[1] (the N = 1 default): whole graph + all features in every GPU's HBM.
-  feature-shard  configs[2] (the N > 1 default): the graph structure in every GPU's HBM, the
-                 feature rows sharded v mod N over the GPUs behind the P2P feature server
-                 (remote rows read one-sided over xGMI through IPC-mapped peer memory; setup
-                 collectives over RCCL).
+  hot-shard      configs[2] (the N > 1 default): the graph structure in every GPU's HBM; a
+                 hot-node feature cache (the --hot-frac highest in-degree nodes) on every GPU and
+                 the other feature rows sharded v mod N behind the P2P feature server (remote
+                 rows read one-sided over xGMI through IPC-mapped peer memory; setup collectives
+                 over RCCL).  The reference's cache planner gives each GPU its hot nodes and pools
+                 the rest (cache_value.py:65-150, 277-308).
+  feature-shard  the same with no hot cache: every feature row sharded v mod N.
   shard          structure and features both sharded v mod N (neighbour lists read over xGMI
                  too: the configs[4] "gather + xGMI p2p" stress layout).
 --cache-frac f < 1 keeps only the ceil(f*N) highest in-degree nodes in HBM (sharded by rank in
@@ -29,7 +32,8 @@ node_classification.py:325-328).  Every rank samples its own slice of the train 
 loop has no collective.  value = sampled edges of all ranks / max-over-ranks time.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--scale S --ef E]
-                       [--mode replicated|feature-shard|shard] [--bias] [--cache-frac f]
+                       [--mode replicated|hot-shard|feature-shard|shard] [--hot-frac h]
+                       [--bias] [--cache-frac f]
 """
 import argparse
 import json
@@ -52,7 +56,8 @@ XGMI_LINK_GBPS = 153.0  # one xGMI link per peer
 # the SURVEY 8(d) synthetic shapes by RMAT (scale, edge factor)
 WORKLOADS = {(17, 9): "arxiv-like", (21, 59): "products-like", (27, 12): "papers100M-like",
              (26, 16): "RMAT-1B"}
-CONFIG_OF_MODE = {"replicated": "configs[1]", "feature-shard": "configs[2]",
+CONFIG_OF_MODE = {"replicated": "configs[1]", "hot-shard": "configs[2]",
+                  "feature-shard": "configs[2] without its hot cache",
                   "shard": "configs[4] layout"}
 
 
@@ -71,8 +76,11 @@ def parse(argv=None):
     p.add_argument("--scale", type=int, default=21)   # products-like: 2,097,152 nodes
     p.add_argument("--ef", type=int, default=59)      # 123.7 M edges
     p.add_argument("--dim", type=int, default=100)
-    p.add_argument("--mode", choices=["auto", "replicated", "feature-shard", "shard"],
-                   default="auto", help="auto = replicated at N = 1, feature-shard at N > 1")
+    p.add_argument("--mode", default="auto",
+                   choices=["auto", "replicated", "hot-shard", "feature-shard", "shard"],
+                   help="auto = replicated at N = 1, hot-shard at N > 1")
+    p.add_argument("--hot-frac", type=float, default=0.2,
+                   help="hot-shard: share of nodes (highest in-degree) cached on every GPU")
     p.add_argument("--shard", action="store_true", help="alias of --mode shard")
     p.add_argument("--bias", action="store_true",
                    help="biased (degree-weighted) sampler: probs[e] = 1 + indeg(indices[e])")
@@ -135,16 +143,22 @@ def check_world(args, world_env):
 def resolve_mode(args, world):
     if args.mode != "auto":
         return args.mode
-    return "replicated" if world == 1 else "feature-shard"
+    return "replicated" if world == 1 else "hot-shard"
 
 
-def cache_lists(mode, N, rank, world, hot):
-    """(sampler cache nids, feature cache nids) of this rank."""
+def cache_lists(mode, N, rank, world, hot, hot_feat=None):
+    """(sampler cache nids, feature cache nids) of this rank.  hot: the HBM-cached nodes when
+    only part of the graph is cached (--cache-frac), else None; hot_feat: hot-shard's
+    replicated hot nodes."""
     def shard(all_ids):
         return all_ids[rank::world] if world > 1 else all_ids
     everything = hot if hot is not None else torch.arange(N)
     if mode == "replicated" or world == 1:
         return everything, everything
+    if mode == "hot-shard":
+        cold = torch.ones(N, dtype=torch.bool)
+        cold[hot_feat] = False
+        return everything, torch.cat([hot_feat, shard(torch.nonzero(cold).flatten())])
     if mode == "feature-shard":
         return everything, shard(everything)
     return shard(everything), shard(everything)
@@ -357,6 +371,10 @@ def main():
     N = indptr.numel() - 1
     E = indices.numel()
     hot = hot_set(indices, N, args.cache_frac, dev)
+    if mode == "hot-shard" and hot is not None:
+        raise SystemExit("bench.py: --mode hot-shard caches every row somewhere; it does not "
+                         "combine with --cache-frac")
+    hot_feat = hot_set(indices, N, args.hot_frac, dev) if mode == "hot-shard" else None
     g2 = torch.Generator()
     g2.manual_seed(2)
     train = torch.randperm(N, generator=g2)[: N // 10]
@@ -365,7 +383,10 @@ def main():
         f"({host_copy})")
 
     # ---------------- services
-    s_cache, f_cache = cache_lists(mode, N, rank, world, hot)
+    s_cache, f_cache = cache_lists(mode, N, rank, world, hot, hot_feat)
+    # the rows this GPU holds (the others come from a peer or the host)
+    local_mask = torch.zeros(N, dtype=torch.bool, device=dev)
+    local_mask[f_cache.to(dev)] = True
     # which nodes any GPU holds (the rest are host rows), for the host-row share reported below
     cached_mask = torch.zeros(N, dtype=torch.bool, device=dev)
     cached_mask[(hot if hot is not None else torch.arange(N)).to(dev)] = True
@@ -399,7 +420,7 @@ def main():
         dist, red_dev, elapsed, edges, rows, gather_bytes)
 
     side = side_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, cached_mask,
-                     per_row)
+                     local_mask, per_row)
 
     # roofline of the dominant HBM kernel (feature gather), timed live by its own workgroups
     g_ms = prof["gather_ms"] / max(prof["gather_launches"], 1)
@@ -434,6 +455,11 @@ def main():
     if mode == "replicated":
         placement = ("whole graph + features in HBM" +
                      (" on every GPU (independent replicas)" if world > 1 else ""))
+    elif mode == "hot-shard":
+        placement = (f"graph structure in every GPU's HBM; hot-node feature cache of the "
+                     f"{args.hot_frac:.0%} highest in-degree nodes on every GPU, the other rows "
+                     f"sharded v mod {world} over the GPUs (P2P feature server, remote rows over "
+                     "xGMI)")
     elif mode == "feature-shard":
         placement = (f"graph structure in every GPU's HBM, feature rows sharded v mod {world} "
                      "over the GPUs (P2P feature server, remote rows over xGMI)")
@@ -482,6 +508,8 @@ def main():
         "host_step_gap_ms": step_gaps,
         "allocator_mallocs_in_timed_region": mallocs,
         "host_row_share": side["host_rows"],
+        # gathered rows that cached on another GPU (read over xGMI)
+        "remote_row_share": side["remote_rows"],
         # host rows cross PCIe Gen5 x16 (63 GB/s spec): their read rate during the gather
         "gather_host_read_GBps": (side["host_rows"] * rows * row_bytes /
                                   (prof["gather_ms"] * 1e-3) / 1e9
@@ -553,7 +581,7 @@ def pmc_traffic(dim, rows_per_launch):
 
 
 def side_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, cached_mask,
-              per_row):
+              local_mask, per_row):
     """Outside the timed region: SURVEY 8(d)'s synchronous per-call figures (median of
     --seq-calls device-synchronised calls after 3 warm-ups), the sample call's GPU span, the
     label select kernel, and the feature gather on its own."""
@@ -583,6 +611,8 @@ def side_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, cache
     # share of the gathered rows that are host rows
     host_rows = sum(float((~cached_mask[n.long()]).sum()) / max(n.numel(), 1)
                     for n in side_nids) / max(len(side_nids), 1)
+    remote_rows = sum(float((cached_mask[n.long()] & ~local_mask[n.long()]).sum()) /
+                      max(n.numel(), 1) for n in side_nids) / max(len(side_nids), 1)
     dgs.ops.profile_enable(dgs.ops.PROFILE_GATHER)
     iso_rows = 0
     for n in side_nids:
@@ -605,6 +635,7 @@ def side_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, cache
         "sample_span_ms": sp["sample_ms"] / max(sp["sample_calls"], 1),
         "select_ms": sp["select_ms"] / max(sp["select_launches"], 1),
         "host_rows": host_rows,
+        "remote_rows": remote_rows,
         "iso_gbps": (iso_rows * per_row / (iso["gather_ms"] * 1e-3) / 1e9
                      if iso["gather_ms"] > 0 else 0.0),
         "iso_ms": iso["gather_ms"] / max(iso["gather_launches"], 1),

@@ -66,16 +66,6 @@ int bias_hub_blocks() {
   return n;
 }
 
-// Biased hub workers: 1 = waves (k_bias_hub_wave), 0 = half-waves (k_bias_hub);
-// DGS_BIAS_HUB_WAVE overrides (A/B).
-bool bias_hub_wave() {
-  static const bool w = [] {
-    const char *e = getenv("DGS_BIAS_HUB_WAVE");
-    return e ? atoi(e) != 0 : false;
-  }();
-  return w;
-}
-
 using RowInfo = NodeEntry;  // {absolute neighbour-id pointer, degree | location << 56}
 
 __device__ __forceinline__ int64_t ri_deg(const RowInfo &r) { return r.dl & kOffMask; }
@@ -1166,225 +1156,6 @@ __global__ __launch_bounds__(kTileRows, DGS_BIAS_HUB_WAVES) void k_bias_hub(Bias
   flush(h);
 }
 
-// Wave workers (round 3).  The 64 lanes of a wave take one kBiasChunk-edge chunk per step:
-// lane L = 32 hf + l evaluates edges i = kBiasChunk q + l + 32 (4 hf + t), t < 4, i.e. draws
-// jb_l + 8 q + 4 hf + t of subsequence 32 w + l -- the same coordinates as the half-wave kernel
-// above, so the same keys.  Everything about the row and the chunk is wave-uniform and lives in
-// scalar registers, the Philox key included (its round-key additions become scalar too).  The
-// chunk's 8 draws per l span Philox blocks cb, cb + 1, cb + 2 (cb = (jb_l + 8 q) >> 2): half 0
-// computes cb + 1 and half 1 computes cb + 2, the halves trade them with one v_permlane32_swap
-// per word (half 1 needs cb + 1; half 0 keeps cb + 2, the next chunk's cb), so a wave staying in
-// a row computes one block per lane per chunk, as the half-wave kernel does per two steps.  Each
-// half keeps its own top-k list (the halves see different edges); the filter threshold is the
-// best of both halves' k-th keys and the row's published one, all lower bounds of the row's final
-// k-th key.  At a row's end the halves' lists are merged and flushed to slot (wave + hub).
-__global__ __launch_bounds__(kTileRows, DGS_BIAS_HUB_WAVES) void k_bias_hub_wave(
-    BiasHubArgs a, const int64_t *bsum, int64_t *boff, int64_t *d_nnz) {
-  if (blockIdx.x == 0) {
-    __shared__ int64_t lds[kTileRows / 64];
-    const int64_t nb = (a.Sc.get() + kTileRows - 1) / kTileRows;
-    const int64_t tot = block_scan_range<kTileRows, 8>(bsum, nb, boff, lds);
-    if (threadIdx.x == 0) {
-      boff[nb] = tot;
-      *d_nnz = tot;
-    }
-  }
-  const int64_t S = a.Sc.get();
-  const int64_t G = (S + 15) / 16;
-  const uint64_t packed = (uint64_t)*a.hub.count;
-  const int64_t H = (int64_t)(packed >> kHubShift);
-  if (H == 0) return;
-  const int64_t total = (int64_t)(packed & kHubChunkMask);
-  const int L = threadIdx.x & 63, l = L & 31, hf = L >> 5;
-  const int64_t wk = (int64_t)blockIdx.x * (kTileRows / 64) +
-                     (int64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t nw = bias_workers(total, a.nworkers);
-  if (wk >= nw) return;
-  const int64_t c0 = bias_worker_c0(total, wk, nw);
-  const int64_t c1 = bias_worker_c0(total, wk + 1, nw);
-  if (c0 >= c1) return;
-  const int64_t k = a.k;
-  int64_t h = (int64_t)wave_uniform((uint64_t)group_search<64>(a.hub.cptr, H, c0));
-  int64_t hstart = 0, hnext = 0, deg = 0, jb = 0;
-  const float *pr = nullptr;
-  int32_t published = key_order(-__builtin_inff());
-  uint2 kk;
-  uint32_t sub = 0;
-  HalfTopK top;
-  auto load_row = [&](int64_t hh) {
-    hstart = (int64_t)wave_uniform((uint64_t)a.hub.cptr[hh]);
-    hnext = hh + 1 < H ? (int64_t)wave_uniform((uint64_t)a.hub.cptr[hh + 1]) : total;
-    const int64_t r = (int64_t)wave_uniform((uint64_t)a.hub.row[hh]);
-    deg = (int64_t)wave_uniform((uint64_t)ri_deg(a.rowinfo[r]));
-    pr = reinterpret_cast<const float *>(wave_uniform((uint64_t)a.hub.aux[hh]));
-    const uint64_t key = a.seed * (uint64_t)G + (uint64_t)(r / 16);
-    kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
-    sub = (uint32_t)(32 * ((r % 16) & 3) + l);
-    jb = chain_draws(a.rowinfo, r, k, l);
-    top = HalfTopK();
-    published = key_order(-__builtin_inff());
-  };
-  __shared__ float s_ck[kTileRows / 32][64];
-  __shared__ int32_t s_ci[kTileRows / 32][64];
-  const int hw = threadIdx.x >> 5;
-  int ncand = 0;  // buffered candidates of this half-wave (the same on its 32 lanes)
-  auto merge = [&]() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    while (ncand > 0) {
-      const int n = ncand < 32 ? ncand : 32;
-      const bool v = l < n;
-      const float ck = v ? s_ck[hw][ncand - n + l] : -__builtin_inff();
-      const int32_t ci = v ? s_ci[hw][ncand - n + l] : INT32_MAX;
-      top.push(ck, ci, v, k, l);
-      ncand -= n;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-  // the other half's value of x (lanes 0-31 <-> 32-63)
-  auto other_half = [&](uint32_t x) -> uint32_t {
-    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-    return hf ? r[0] : r[1];
-  };
-  auto flush = [&](int64_t hh) {
-    merge();
-    // the halves' sorted lists merged (the other half's reversed: a bitonic sequence)
-    const float rk = __shfl(top.bk, (L ^ 32) ^ 31, 64);
-    const int32_t ri = __shfl(top.bi, (L ^ 32) ^ 31, 64);
-    if (ares_better(rk, ri, top.bk, top.bi)) {
-      top.bk = rk;
-      top.bi = ri;
-    }
-#pragma unroll
-    for (int stride = 16; stride > 0; stride >>= 1)
-      HalfTopK::cas(top.bk, top.bi, stride, (l & stride) == 0);
-    const int n = __builtin_popcount(half_ballot(l < k && top.bi != INT32_MAX));
-    const int64_t slot = wk + hh;
-    if (hf == 0 && l < n) {
-      a.ckey[slot * k + l] = top.bk;
-      a.cidx[slot * k + l] = top.bi;
-    }
-    if (L == 0) a.ccnt[slot] = n;
-  };
-  load_row(h);
-  const int32_t published_none = key_order(-__builtin_inff());
-  uint32_t carry[4] = {0u, 0u, 0u, 0u};  // half 0: block cb of this chunk (the last one's cb + 2)
-  bool carried = false;
-  for (int64_t c = c0; c < c1; ++c) {
-    while (c >= hnext) {
-      flush(h);
-      ++h;
-      load_row(h);
-      carried = false;
-    }
-    const int64_t q = c - hstart;
-    if (L == 0 && c == hstart) a.wfirst[h] = (int32_t)wk;
-    if (L == 0 && c == hnext - 1) a.wlast[h] = (int32_t)wk;
-    const int32_t shared_ord =
-        (int32_t)__hip_atomic_load(a.hub.thr + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t i0 = (uint32_t)(q * kBiasChunk) + (uint32_t)(l + 128 * hf);
-    const bool whole = q * kBiasChunk + kBiasChunk <= deg;
-    float p[4];
-    {
-      const global_ptr<float> pg = as_global(pr);
-      const uint32_t last = (uint32_t)(deg - 1);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const uint32_t i = i0 + 32u * t;
-        p[t] = pg[whole ? i : (i < last ? i : last)];
-      }
-    }
-    const int64_t j0 = jb + q * 8;  // this l's first draw of the chunk (half 0)
-    const int64_t cb = j0 >> 2;
-    const int off = (int)(j0 & 3);
-    // own block: cb + 1 (half 0) / cb + 2 (half 1)
-    const uint64_t ob = (uint64_t)(cb + 1 + hf);
-    const uint4 own = philox4x32_10(make_uint4((uint32_t)ob, (uint32_t)(ob >> 32), sub, 0u), kk);
-    if (!carried) {
-      // the wave's first chunk in this row: half 0 also needs block cb
-      if (hf == 0) {
-        const uint4 o = philox4x32_10(make_uint4((uint32_t)cb, (uint32_t)((uint64_t)cb >> 32), sub, 0u), kk);
-        carry[0] = o.x;
-        carry[1] = o.y;
-        carry[2] = o.z;
-        carry[3] = o.w;
-      }
-    }
-    const uint32_t ownw[4] = {own.x, own.y, own.z, own.w};
-    uint32_t wv[8];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const uint32_t got = other_half(ownw[e]);  // half 0: cb + 2; half 1: cb + 1
-      wv[e] = hf ? got : carry[e];
-      wv[4 + e] = ownw[e];
-      carry[e] = got;  // half 0: the next chunk's cb (half 1's carry is unused)
-    }
-    carried = true;
-    const uint32_t m2 = (off & 2) ? ~0u : 0u, m1 = (off & 1) ? ~0u : 0u;
-    uint32_t w2[5];
-#pragma unroll
-    for (int e = 0; e < 5; ++e) w2[e] = bitsel(m2, wv[e + 2], wv[e]);
-#pragma unroll
-    for (int e = 0; e < 5; ++e) asm volatile("" ::"v"(w2[e]));
-    // filter threshold: the best of both halves' k-th keys and the row's published one
-    const int32_t mine_ord = top.filtering(k) ? key_order(top.thr_k) : published_none;
-    const int32_t both = max(mine_ord, (int32_t)other_half((uint32_t)mine_ord));
-    const int32_t thr_ord = max(both, shared_ord);
-    bool filter = thr_ord != published_none;
-    float thr_s = slack_thr(key_from_order(thr_ord));
-    const uint32_t deg32 = (uint32_t)deg;
-    float u[4];
-    uint32_t m = 0;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      u[t] = curand_uniform_from(bitsel(m1, w2[t + 1], w2[t]));
-      const bool valid = whole | (i0 + 32u * t < deg32);
-      m |= (uint32_t)(valid & (!filter | ares_may_pass_s(u[t], p[t], thr_s))) << t;
-    }
-    while (half_ballot(m != 0)) {
-      const bool has = m != 0;
-      const int t = has ? __builtin_ctz(m) : 0;
-      m &= m - 1;
-      float ut = u[0], pt = p[0];
-#pragma unroll
-      for (int e = 1; e < 4; ++e) {
-        ut = t == e ? u[e] : ut;
-        pt = t == e ? p[e] : pt;
-      }
-      const float key = has ? ares_key(ut, pt) : -__builtin_inff();
-      const int32_t it = (int32_t)(i0 + 32u * t);
-      const bool keep = has && ares_better(key, it, top.thr_k, top.thr_i);
-      const uint32_t b = half_ballot(keep);
-      if (keep) {
-        const int pos = ncand + __builtin_popcount(b & ((1u << l) - 1u));
-        s_ck[hw][pos] = key;
-        s_ci[hw][pos] = it;
-      }
-      ncand += __builtin_popcount(b);
-      if (ncand >= 32) merge();
-      if (!filter && top.filtering(k)) {
-        filter = true;
-        thr_s = slack_thr(top.thr_k);
-        uint32_t keep2 = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) keep2 |= (uint32_t)ares_may_pass_s(u[e], p[e], thr_s) << e;
-        m &= keep2;
-      }
-    }
-    // publish the wave's best k-th key when it improved on what it last published
-    const int32_t mine2 = top.filtering(k) ? key_order(top.thr_k) : published_none;
-    const int32_t best = max(mine2, (int32_t)other_half((uint32_t)mine2));
-    if (best != published_none && best > published && best > shared_ord) {
-      if (L == 0) atomicMax((long long *)(a.hub.thr + h), (long long)best);
-      published = best;
-    }
-  }
-  flush(h);
-}
-
 #ifndef DGS_MERGE_HALF_SLOTS
 #define DGS_MERGE_HALF_SLOTS 8
 #endif
@@ -1403,19 +1174,42 @@ __device__ __forceinline__ void merge_slots(const BiasHubArgs &a, HalfTopK &top,
   // a worker's list is sorted (descending); the second list of a pair is read in reverse
   // so the 32 lanes hold a bitonic sequence
   const int er = part ? 15 - e : e;
-  for (int64_t w0 = wf + (int64_t)per * first; w0 <= wl; w0 += step * per) {
+  // A batch's count and entries are loaded together (the entry address does not wait for the
+  // count: lanes past the count are masked afterwards), and the next batch's loads go out before
+  // the current batch is merged, so a long slot list pays about one load latency in all instead
+  // of two per batch (round 3).
+  const int erc = er < (int)k ? er : (int)k - 1;  // inside this slot's k entries
+  auto fetch = [&](int64_t w0, int &n, float &key_i, int32_t &i) {
     const int64_t w = w0 + part;
-    bool have = w <= wl && bias_worker_c0(total, w, nw) != bias_worker_c0(total, w + 1, nw);
-    const int64_t slot = w + h;
-    const int n = have ? a.ccnt[slot] : 0;
+    const bool have =
+        w <= wl && bias_worker_c0(total, w, nw) != bias_worker_c0(total, w + 1, nw);
+    const int64_t slot = (have ? w : wf) + h;  // a valid slot either way
+    n = a.ccnt[slot];
+    key_i = a.ckey[slot * k + erc];
+    i = a.cidx[slot * k + erc];
+    if (!have) n = 0;
+  };
+  const int64_t stride = step * per;
+  int64_t w0 = wf + (int64_t)per * first;
+  if (w0 > wl) return;
+  int n;
+  float key_i;
+  int32_t i;
+  fetch(w0, n, key_i, i);
+  for (;;) {
+    const int64_t wn = w0 + stride;
+    int n2 = 0;
+    float key2 = -__builtin_inff();
+    int32_t i2 = INT32_MAX;
+    if (wn <= wl) fetch(wn, n2, key2, i2);
     const bool valid = er < n;
-    float key_i = -__builtin_inff();
-    int32_t i = INT32_MAX;
-    if (valid) {
-      key_i = a.ckey[slot * k + er];
-      i = a.cidx[slot * k + er];
-    }
-    top.push_bitonic(key_i, i, valid, k, l, per == 1);
+    top.push_bitonic(valid ? key_i : -__builtin_inff(), valid ? i : INT32_MAX, valid, k, l,
+                     per == 1);
+    if (wn > wl) break;
+    w0 = wn;
+    n = n2;
+    key_i = key2;
+    i = i2;
   }
 }
 
@@ -1544,7 +1338,8 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   int32_t *tpre = ws.tpre.as<int32_t>();
   int32_t *tpre2 = tpre + S;
   if (use_hubs) ws.hubslot.ensure(sizeof(int32_t) * (size_t)(S * k));
-  const PrepArgs pa{src, seeds, Sc, k, (int)replace, use_hubs ? 1 : (bias_hubs ? 2 : 0),
+  const PrepArgs pa{src, seeds, Sc, k, (int)replace,
+                    use_hubs ? 1 : (bias_hubs ? 2 : 0),
                     (int)bias_replace, rowinfo, tpre, tpre2, bsum, tsum, hub,
                     ws.hubslot.as<int32_t>(), table, next_count};
   if (tail)
@@ -1587,8 +1382,7 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     DGS_CHECK(k <= 32, "biased sampling supports num_picks <= 32 (rowwise_sampling_bias.cu:73)");
     float *cdf = nullptr;
     const dim3 grid((unsigned)ceil_div(S, kBiasRowsPerBlock));
-    const bool wave_workers = bias_hub_wave();
-    const int64_t nworkers = (int64_t)bias_hub_blocks() * (kTileRows / (wave_workers ? 64 : 32));
+    const int64_t nworkers = (int64_t)bias_hub_blocks() * (kTileRows / 32);
     BiasHubArgs ba{};
     if (bias_hubs) {
       const int64_t slots = nworkers + S;
@@ -1600,12 +1394,8 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
       int32_t *wfirst = ccnt + slots;
       ba = BiasHubArgs{src, Sc, k, launch_seed, rowinfo, tpre, boff, hub, ckey, cidx, ccnt,
                        wfirst, wfirst + S, nworkers, rowpos, col, table};
-      if (wave_workers)
-        hipLaunchKernelGGL(k_bias_hub_wave, dim3(bias_hub_blocks()), dim3(kTileRows), 0, st, ba,
-                           (const int64_t *)bsum, boff, d_nnz);
-      else
-        hipLaunchKernelGGL(k_bias_hub, dim3(bias_hub_blocks()), dim3(kTileRows), 0, st, ba,
-                           (const int64_t *)bsum, boff, d_nnz);
+      hipLaunchKernelGGL(k_bias_hub, dim3(bias_hub_blocks()), dim3(kTileRows), 0, st, ba,
+                         (const int64_t *)bsum, boff, d_nnz);
       DGS_LAUNCH_CHECK();
     }
     if (replace) {
@@ -1619,6 +1409,18 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
                          launch_seed, rowinfo, tpre, boff, tpre2, tboff, cdf, rowpos, col, table,
                          (const int64_t *)nullptr);
     } else {
+      // DGS_BIAS_SPLIT_MERGE=1: rows and hub merge as two launches (profiling)
+      static const bool split = getenv("DGS_BIAS_SPLIT_MERGE") != nullptr;
+      if (bias_hubs && split) {
+        hipLaunchKernelGGL(k_sample_bias<false>, grid, dim3(kTileRows), 0, st, src, Sc, k,
+                           launch_seed, rowinfo, tpre, boff, tpre2, tboff, cdf, rowpos, col,
+                           table, (const int64_t *)hub.hubid);
+        DGS_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_bias_hub_merge, dim3((unsigned)std::min<int64_t>(S, 2048)),
+                           dim3(kTileRows), 0, st, ba);
+        DGS_LAUNCH_CHECK();
+        return;
+      }
       if (bias_hubs) {
         const int64_t mb = std::min<int64_t>(S, 2048);
         hipLaunchKernelGGL(k_bias_rows_merge, dim3((unsigned)(grid.x + mb)), dim3(kTileRows), 0,

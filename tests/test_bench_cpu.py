@@ -32,7 +32,7 @@ def test_spawn_refuses_more_ranks_than_gpus(monkeypatch):
 
 def test_modes_and_cache_lists():
     assert bench.resolve_mode(bench.parse([]), 1) == "replicated"
-    assert bench.resolve_mode(bench.parse(["--gpus", "8"]), 8) == "feature-shard"
+    assert bench.resolve_mode(bench.parse(["--gpus", "8"]), 8) == "hot-shard"
     assert bench.parse(["--shard"]).mode == "shard"
     N, W = 37, 4
     allv = torch.arange(N)
@@ -49,6 +49,18 @@ def test_modes_and_cache_lists():
     # the union of the sharded feature lists is every node exactly once
     parts = torch.cat([bench.cache_lists("feature-shard", N, r, W, None)[1] for r in range(W)])
     assert torch.equal(torch.sort(parts).values, allv)
+    # hot-shard: the hot nodes on every GPU, every other node on exactly one
+    hot_feat = torch.tensor([4, 17, 30])
+    seen = torch.zeros(N, dtype=torch.int64)
+    for r in range(W):
+        s, f = bench.cache_lists("hot-shard", N, r, W, None, hot_feat)
+        assert torch.equal(s, allv) and torch.equal(f[:3], hot_feat)
+        assert torch.unique(f).numel() == f.numel()
+        seen[f] += 1
+    assert torch.equal(seen[hot_feat], torch.full((3,), W))
+    cold = torch.ones(N, dtype=torch.bool)
+    cold[hot_feat] = False
+    assert torch.equal(seen[cold], torch.ones(int(cold.sum()), dtype=torch.int64))
 
 
 def test_workload_names():
