@@ -87,6 +87,8 @@ struct RowSrc {
   int64_t num_nodes;
   int64_t *bad;
   int64_t bad_tag;
+  // Edges of the whole graph (bounds the biased hub candidate lists of one hop); 0 = unknown.
+  int64_t num_edges;
 };
 
 struct HopScratch {

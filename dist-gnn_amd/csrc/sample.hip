@@ -66,6 +66,25 @@ int bias_hub_blocks() {
   return n;
 }
 
+// Biased hub rows: streaming scheme (default) or the chunked one (DGS_BIAS_STREAM=0, A/B).
+bool bias_stream_on() {
+  static const bool on = [] {
+    const char *e = getenv("DGS_BIAS_STREAM");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+constexpr int kBiasStreamBlocks = 1024;
+// Workgroups of the streaming kernel; DGS_BIAS_STREAM_BLOCKS overrides.
+int bias_stream_blocks() {
+  static const int n = [] {
+    const char *e = getenv("DGS_BIAS_STREAM_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : kBiasStreamBlocks;
+  }();
+  return n;
+}
+
 using RowInfo = NodeEntry;  // {absolute neighbour-id pointer, degree | location << 56}
 
 __device__ __forceinline__ int64_t ri_deg(const RowInfo &r) { return r.dl & kOffMask; }
@@ -159,6 +178,44 @@ __device__ __forceinline__ float key_from_order(int32_t m) {
   return __int_as_float(m >= 0 ? m : (m ^ 0x7FFFFFFF));
 }
 
+// Biased hub rows, streaming scheme (see k_bias_boot / k_bias_stream below): a threshold from
+// a spread sample of 8 x kBiasSampleSteps 32-edge steps (4096 edges), then every edge is tested
+// against it.
+#ifndef DGS_BIAS_SAMPLE_STEPS
+#define DGS_BIAS_SAMPLE_STEPS 16
+#endif
+constexpr int64_t kBiasSampleSteps = DGS_BIAS_SAMPLE_STEPS;
+// Steps per streamed chunk (a chunk = 32 kStreamT edges; one new Philox block per 4 steps).
+#ifndef DGS_BIAS_STREAM_T
+#define DGS_BIAS_STREAM_T 4
+#endif
+constexpr int kStreamT = DGS_BIAS_STREAM_T;
+constexpr int kStreamChunk = 32 * kStreamT;
+static_assert(kStreamT % 4 == 0, "whole Philox blocks per chunk");
+// Candidate room of the streamed rows.  The sample threshold lets about k * deg / P of a row's
+// edges through (P = min(deg, 4096) sampled edges), i.e. about k for rows the sample covers and
+// k / 32 per 128-edge chunk for larger ones.  The room is linear in the row's chunk range, so it
+// is addressed from the chunk offset the hub registration already returns (no second counter):
+// 16 kk per hub plus kk / 4 per chunk, kk = max(k, 8): >= 8x the expectation (small k is sized
+// as 8: the spread of a small order statistic is wider).  A row that overflows is recomputed
+// exactly (slow, rare).
+__host__ __device__ __forceinline__ int64_t bias_room_start(int64_t h, int64_t chunk, int64_t k) {
+  const int64_t kk = k < 8 ? 8 : k;
+  return 16 * kk * h + kk * chunk / 4;
+}
+
+// Per-hub candidate lists of the streaming scheme: hub h owns key/idx[base[h], base[h] +
+// cap[h]); cnt[h] counts appends (> cap[h]: overflowed, recomputed by the merge).
+struct BiasCand {
+  int32_t *cnt;
+  int32_t *cap;
+  int64_t *base;
+  float *key;
+  int32_t *idx;
+  int64_t limit;                // entries of key / idx
+  int64_t cap_max;              // test hook (DGS_BIAS_TEST_CAP): caps every streamed row's room
+};
+
 // ------------------------------------------------------------------------------------
 // Prep: per-row lookup (one 16-byte node-table load), per-row in-tile output prefix, tile
 // sums, hub detection (+ hub slot initialisation, slot s = s: rowwise_sampling.cu:80-82).
@@ -179,6 +236,7 @@ struct PrepArgs {
   int32_t *hubslot;
   Table table;
   int64_t *next_hub_count;
+  BiasCand cand;  // biased hubs, streaming scheme (cand.cnt == nullptr: chunked scheme)
 };
 
 __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
@@ -210,7 +268,8 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
       const bool is_hub = a.use_hubs == 1 ? deg - k > kHubT : deg > kBiasHubT;
       if (is_hub) {
         const uint64_t nch = a.use_hubs == 1 ? (uint64_t)(deg - k + 511) / 512
-                                             : (uint64_t)(deg + kBiasChunk - 1) / kBiasChunk;
+                             : a.cand.cnt   ? (uint64_t)(deg + kStreamChunk - 1) / kStreamChunk
+                                            : (uint64_t)(deg + kBiasChunk - 1) / kBiasChunk;
         const uint64_t old = atomicAdd((unsigned long long *)a.hub.count,
                                        (unsigned long long)((uint64_t(1) << kHubShift) | nch));
         h = (int64_t)(old >> kHubShift);
@@ -222,6 +281,16 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
         } else {
           a.hub.thr[h] = key_order(-__builtin_inff());
           a.hub.aux[h] = (int64_t)row_probs(a.src, ri);
+          if (a.cand.cnt) {
+            const int64_t c0 = (int64_t)(old & kHubChunkMask);
+            const int64_t b = bias_room_start(h, c0, k);
+            int64_t cap = bias_room_start(h + 1, c0 + (int64_t)nch, k) - b;
+            if (cap > a.cand.cap_max) cap = a.cand.cap_max;
+            if (b + cap > a.cand.limit) cap = 0;  // out of room: recomputed
+            a.cand.base[h] = b;
+            a.cand.cap[h] = (int32_t)cap;
+            a.cand.cnt[h] = 0;
+          }
         }
       }
       a.hub.hubid[i] = h;
@@ -907,6 +976,7 @@ struct BiasHubArgs {
   int64_t *rowpos;
   int64_t *col;
   Table table;
+  BiasCand cand;  // streaming scheme (cand.cnt != nullptr)
 };
 
 // draws lane l made on the earlier rows of row r's (block, warp) chain (no replacement)
@@ -1282,9 +1352,450 @@ __device__ __forceinline__ void bias_merge_block(const BiasHubArgs &a, int64_t b
   }
 }
 
+__device__ __forceinline__ void stream_merge_block(const BiasHubArgs &a, int64_t blk,
+                                                   int64_t nblk);
 __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
   latency_prio();
-  bias_merge_block(a, blockIdx.x, gridDim.x);
+  if (a.cand.cnt)
+    stream_merge_block(a, blockIdx.x, gridDim.x);
+  else
+    bias_merge_block(a, blockIdx.x, gridDim.x);
+}
+
+// ------------------------------------------------------------------------------------
+// Biased hub rows, streaming scheme (round 3).  The chunked scheme above keeps a running top-k
+// per half-wave worker: 112 VGPRs, 4 waves per SIMD, and its per-edge loop waits on probability
+// and threshold loads it can not hide (0.41 T edges/s against ~1 T for the same Philox +
+// filter work VALU-bound).  Here the work is split so the per-edge pass holds no top-k state:
+//   k_bias_boot    one workgroup per hub row: over a spread sample (8 runs of kBiasSampleSteps
+//                  steps, 4096 edges) each lane keeps the largest key_lower() (a provable
+//                  lower bound of the exact key, from the hardware log2); the k-th largest of
+//                  the 256 lane maxima is a lower bound T of the row's final k-th key.
+//   k_bias_stream  every edge of the row: Philox and the cheap log2 bound against T; the few
+//                  that pass go to the row's candidate list as (u, edge).  The bound is
+//                  conservative, so every final pick is kept (they all have key >= final k-th
+//                  >= T).  Half-wave workers over contiguous 128-edge chunk ranges, Philox blocks
+//                  carried across a worker's chunks, no LDS, no exact key (registers).
+//   merge          (in k_bias_rows_merge) exact keys of each row's candidates and their top-k;
+//                  a row whose list overflowed (or whose sample had no finite k-th key) is
+//                  recomputed exactly.
+// Every edge's key comes from its reference coordinates, so the picks are those of the chunked
+// scheme (and of the oracle), bit for bit.
+
+struct HubRowCtx {
+  int64_t r, deg;
+  global_ptr<float> pr;
+  uint2 kk;
+  uint32_t sub;
+  int64_t jb;
+};
+__device__ __forceinline__ HubRowCtx hub_row_ctx(const BiasHubArgs &a, int64_t h, int64_t G,
+                                                 int l) {
+  HubRowCtx c;
+  c.r = a.hub.row[h];
+  c.deg = ri_deg(a.rowinfo[c.r]);
+  c.pr = as_global(reinterpret_cast<const float *>(a.hub.aux[h]));
+  const uint64_t key = a.seed * (uint64_t)G + (uint64_t)(c.r / 16);
+  c.kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
+  c.sub = (uint32_t)(32 * ((c.r % 16) & 3) + l);
+  c.jb = chain_draws(a.rowinfo, c.r, a.k, l);
+  return c;
+}
+
+// Steps [s0, s1) of a row (step s: edge i = 32 s + l, draw jb + s of the lane's subsequence) into
+// `top`: a two-block Philox window refilled once per 4 steps (the loop of sample_bias_block),
+// exact keys for the edges the cheap bound lets through.
+__device__ __forceinline__ void bias_run(const HubRowCtx &c, int64_t s0, int64_t s1, int64_t k,
+                                         int l, HalfTopK &top) {
+  const int64_t n = s1 - s0;
+  if (n <= 0) return;
+  const int64_t j = c.jb + s0;
+  const int64_t bl = j >> 2;
+  const int off = (int)(j & 3);
+  const uint32_t m2 = (off & 2) ? ~0u : 0u, m1 = (off & 1) ? ~0u : 0u;
+  uint4 A = philox4x32_10(make_uint4((uint32_t)bl, (uint32_t)((uint64_t)bl >> 32), c.sub, 0u),
+                          c.kk);
+  bool filter = top.filtering(k);
+  float thr_s = filter ? slack_thr(top.thr_k) : -__builtin_inff();
+  const int64_t e0 = 32 * s0 + l;
+  const int64_t e1 = 32 * s1 < c.deg ? 32 * s1 : c.deg;
+  float pn[4];
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) {
+    const int64_t i = e0 + 32 * s4;
+    pn[s4] = i < e1 ? c.pr[i] : 0.0f;
+  }
+  for (int64_t g = 0; 4 * g < n; ++g) {
+    float p[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      p[s4] = pn[s4];
+      const int64_t i = e0 + 128 * (g + 1) + 32 * s4;
+      pn[s4] = i < e1 ? c.pr[i] : 0.0f;
+    }
+    const uint64_t qb = (uint64_t)(bl + g + 1);
+    const uint4 B = philox4x32_10(make_uint4((uint32_t)qb, (uint32_t)(qb >> 32), c.sub, 0u), c.kk);
+    const uint32_t wv[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+    uint32_t w2[5];
+#pragma unroll
+    for (int e = 0; e < 5; ++e) w2[e] = bitsel(m2, wv[e + 2], wv[e]);
+    float u[4];
+    uint32_t mk = 0;
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      u[s4] = curand_uniform_from(bitsel(m1, w2[s4 + 1], w2[s4]));
+      const bool valid = e0 + 128 * g + 32 * s4 < e1;
+      mk |= (uint32_t)(valid & (!filter | ares_may_pass_s(u[s4], p[s4], thr_s))) << s4;
+    }
+    while (half_ballot(mk != 0)) {
+      const bool has = mk != 0;
+      const int t = has ? __builtin_ctz(mk) : 0;
+      mk &= mk - 1;
+      float ut = u[0], pt = p[0];
+#pragma unroll
+      for (int e = 1; e < 4; ++e) {
+        ut = t == e ? u[e] : ut;
+        pt = t == e ? p[e] : pt;
+      }
+      top.push(has ? ares_key(ut, pt) : -__builtin_inff(), (int32_t)(e0 + 128 * g + 32 * t), has,
+               k, l);
+      if (!filter && top.filtering(k)) {
+        filter = true;
+        thr_s = slack_thr(top.thr_k);
+        uint32_t keep = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) keep |= (uint32_t)ares_may_pass_s(u[e], p[e], thr_s) << e;
+        mk &= keep;
+      }
+    }
+    if (top.filtering(k)) {
+      filter = true;
+      thr_s = slack_thr(top.thr_k);
+    }
+    A = B;
+  }
+}
+
+// The 8 half-waves' sorted lists (only the first k of each count) merged pairwise in LDS; the
+// k best, sorted, end in s_key[0][0..k) / s_idx[0][0..k).  Every thread of the workgroup calls.
+__device__ __forceinline__ void tree_merge8(const HalfTopK &top, int64_t k, int g, int l,
+                                            float (*s_key)[32], int32_t (*s_idx)[32]) {
+  const bool mine = l < k && top.bi != INT32_MAX;
+  s_key[g][l] = mine ? top.bk : -__builtin_inff();
+  s_idx[g][l] = mine ? top.bi : INT32_MAX;
+  __syncthreads();
+#pragma unroll
+  for (int step = 1; step < 8; step <<= 1) {
+    if ((g & (2 * step - 1)) == 0) {
+      float mk = s_key[g][l];
+      int32_t mi = s_idx[g][l];
+      const float ok = s_key[g + step][31 - l];
+      const int32_t oi = s_idx[g + step][31 - l];
+      if (ares_better(ok, oi, mk, mi)) {
+        mk = ok;
+        mi = oi;
+      }
+#pragma unroll
+      for (int stride = 16; stride > 0; stride >>= 1) HalfTopK::cas(mk, mi, stride, (l & stride) == 0);
+      s_key[g][l] = mk;
+      s_idx[g][l] = mi;
+    }
+    __syncthreads();
+  }
+}
+
+// A value <= ares_key(u, p) for every u in (0, 1] and p: the hardware log2 (v_log_f32, within a
+// few ulp of dgs_log2f) lowered by 2^-16 relative + 2^-16 absolute, divided through the hardware
+// reciprocal and lowered by another 2^-16 relative -- margins far above every rounding on the way
+// (< 2^-21 relative), so the result lies below RN(dgs_log2f(u) / p).  p outside [2^-100, 2^100]
+// (or not > 0) gives -inf, which keeps every intermediate a normal float.
+__device__ __forceinline__ float key_lower(float u, float p) {
+  const float L = __builtin_amdgcn_logf(u);
+  const float Ll = L - __builtin_fabsf(L) * 1.52587890625e-05f - 1.52587890625e-05f;
+  const float q = Ll * __builtin_amdgcn_rcpf(p) * 1.0000152587890625f;
+  return ((p >= 7.888609052210118e-31f) & (p <= 1.2676506002282294e+30f)) ? q : -__builtin_inff();
+}
+
+// Largest key_lower() of this lane's edges in steps [s0, s1) of a row (the Philox window of
+// bias_run; no cross-lane work).  Any value of it is a real edge's lower bound, so the k-th
+// largest over lanes is at most the k-th largest exact key of the sampled edges.
+__device__ __forceinline__ float lane_max_run(const HubRowCtx &c, int64_t s0, int64_t s1, int l) {
+  float best = -__builtin_inff();
+  const int64_t n = s1 - s0;
+  if (n <= 0) return best;
+  const int64_t j = c.jb + s0;
+  const int64_t bl = j >> 2;
+  const int off = (int)(j & 3);
+  const uint32_t m2 = (off & 2) ? ~0u : 0u, m1 = (off & 1) ? ~0u : 0u;
+  uint4 A = philox4x32_10(make_uint4((uint32_t)bl, (uint32_t)((uint64_t)bl >> 32), c.sub, 0u),
+                          c.kk);
+  const int64_t e0 = 32 * s0 + l;
+  const int64_t e1 = 32 * s1 < c.deg ? 32 * s1 : c.deg;
+  for (int64_t g = 0; 4 * g < n; ++g) {
+    float p[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const int64_t i = e0 + 128 * g + 32 * s4;
+      p[s4] = i < e1 ? c.pr[i] : 0.0f;
+    }
+    const uint64_t qb = (uint64_t)(bl + g + 1);
+    const uint4 B = philox4x32_10(make_uint4((uint32_t)qb, (uint32_t)(qb >> 32), c.sub, 0u), c.kk);
+    const uint32_t wv[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const uint32_t w0 = bitsel(m2, wv[s4 + 2], wv[s4]), w1 = bitsel(m2, wv[s4 + 3], wv[s4 + 1]);
+      const float kl = key_lower(curand_uniform_from(bitsel(m1, w1, w0)), p[s4]);
+      best = e0 + 128 * g + 32 * s4 < e1 ? fmaxf(best, kl) : best;
+    }
+    A = B;
+  }
+  return best;
+}
+
+// 32 floats across a half-wave sorted descending (bitonic network).
+__device__ __forceinline__ float sort32_desc(float v, int l) {
+#pragma unroll
+  for (int size = 2; size <= 32; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const float o = __shfl_xor(v, stride, 32);
+      const bool desc = (l & size) == 0 || size == 32;
+      const bool lower = (l & stride) == 0;
+      v = (desc == lower) ? fmaxf(v, o) : fminf(v, o);
+    }
+  }
+  return v;
+}
+
+// One workgroup per hub row (grid-stride over the hub list): the row's threshold T.  Half-wave g
+// samples kBiasSampleSteps steps from step ns * g / 8 (the whole row when it has fewer than
+// 8 kBiasSampleSteps steps); the 8 sorted lists of lane maxima are merged pairwise in LDS and
+// the k-th largest of the 256 is T.
+__global__ __launch_bounds__(kTileRows) void k_bias_boot(BiasHubArgs a) {
+  latency_prio();
+  __shared__ float s_max[8][32];
+  const int64_t S = a.Sc.get();
+  const int64_t G = (S + 15) / 16;
+  const int64_t H = (int64_t)((uint64_t)*a.hub.count >> kHubShift);
+  const int l = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int64_t k = a.k;
+  for (int64_t h = blockIdx.x; h < H; h += gridDim.x) {
+    const HubRowCtx c = hub_row_ctx(a, h, G, l);
+    const int64_t ns = (c.deg + 31) / 32;
+    const int64_t s0 = ns * g / 8;
+    const int64_t s1 = ns >= 8 * kBiasSampleSteps ? s0 + kBiasSampleSteps : ns * (g + 1) / 8;
+    s_max[g][l] = sort32_desc(lane_max_run(c, s0, s1, l), l);
+    __syncthreads();
+#pragma unroll
+    for (int step = 1; step < 8; step <<= 1) {
+      if ((g & (2 * step - 1)) == 0) {
+        // the top 32 of two descending lists: a bitonic sequence, then one bitonic merge
+        float v = fmaxf(s_max[g][l], s_max[g + step][31 - l]);
+#pragma unroll
+        for (int stride = 16; stride > 0; stride >>= 1) {
+          const float o = __shfl_xor(v, stride, 32);
+          v = (l & stride) == 0 ? fmaxf(v, o) : fminf(v, o);
+        }
+        s_max[g][l] = v;
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == k - 1) a.hub.thr[h] = key_order(s_max[0][k - 1]);
+    __syncthreads();
+  }
+}
+
+// Every edge of the streamed hub rows against the row's boot threshold T.  Its workgroup 0 first
+// does the hop's tile-offset scan (the rows / merge launch after it reads boff).  Row state is
+// kept in 32 bits (a row has < 2^31 edges, a lane's draw offset < 2^28, the hop's chunk count
+// and candidate room < 2^31): register pressure, not arithmetic, sets this kernel's occupancy.
+__global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const int64_t *bsum,
+                                                           int64_t *boff, int64_t *d_nnz) {
+  if (blockIdx.x == 0) {
+    __shared__ int64_t lds[kTileRows / 64];
+    const int64_t nb = (a.Sc.get() + kTileRows - 1) / kTileRows;
+    const int64_t tot = block_scan_range<kTileRows, 8>(bsum, nb, boff, lds);
+    if (threadIdx.x == 0) {
+      boff[nb] = tot;
+      *d_nnz = tot;
+    }
+  }
+  const int64_t S = a.Sc.get();
+  const int64_t G = (S + 15) / 16;
+  const uint64_t packed = (uint64_t)*a.hub.count;
+  const int64_t H = (int64_t)(packed >> kHubShift);
+  const int64_t total = (int64_t)(packed & kHubChunkMask);
+  if (H == 0 || total == 0) return;
+  const int l = threadIdx.x & 31;
+  const int64_t wk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 5;
+  const int64_t nw = bias_workers(total, a.nworkers);
+  if (wk >= nw) return;
+  const uint32_t c0 = (uint32_t)bias_worker_c0(total, wk, nw);
+  const uint32_t c1 = (uint32_t)bias_worker_c0(total, wk + 1, nw);
+  if (c0 >= c1) return;
+  int64_t h = group_search<32>(a.hub.cptr, H, c0);
+  uint32_t hstart = 0, hnext = 0, deg = 0, jb = 0, sub = 0, cb = 0;
+  int32_t cap = 0;
+  global_ptr<float> pr = nullptr;
+  uint2 kk;
+  float T = 0.0f, thr_s = 0.0f;
+  bool skip = false;
+  auto load_row = [&](int64_t hh) {
+    hstart = (uint32_t)a.hub.cptr[hh];
+    hnext = hh + 1 < H ? (uint32_t)a.hub.cptr[hh + 1] : (uint32_t)total;
+    const HubRowCtx c = hub_row_ctx(a, hh, G, l);
+    deg = (uint32_t)c.deg;
+    jb = (uint32_t)c.jb;
+    sub = c.sub;
+    kk = c.kk;
+    pr = c.pr;
+    T = key_from_order((int32_t)a.hub.thr[hh]);
+    thr_s = slack_thr(T);
+    // no finite sample threshold (weights <= 0): every edge would be a candidate; the merge
+    // recomputes the row instead (every worker of the row stores the same marker)
+    skip = !(T > -__builtin_inff());
+    if (skip && l == 0) a.cand.cnt[hh] = INT32_MAX;
+    cb = (uint32_t)a.cand.base[hh];
+    cap = a.cand.cap[hh];
+  };
+  load_row(h);
+  uint32_t carry[4] = {0u, 0u, 0u, 0u};
+  uint32_t carry_cb = ~0u;
+  for (uint32_t ch = c0; ch < c1; ++ch) {
+    while (ch >= hnext) {
+      ++h;
+      load_row(h);
+      carry_cb = ~0u;
+    }
+    if (skip) continue;
+    const uint32_t q = ch - hstart;
+    const uint32_t i0 = q * kStreamChunk + l;
+    const bool whole = q * kStreamChunk + kStreamChunk <= deg;
+    float p[kStreamT];
+#pragma unroll
+    for (int t = 0; t < kStreamT; ++t) {
+      const uint32_t i = i0 + 32u * t;
+      p[t] = pr[whole ? i : (i < deg - 1u ? i : deg - 1u)];
+    }
+    const uint32_t j0 = jb + q * kStreamT;
+    const uint32_t bc = j0 >> 2;
+    const int off = (int)(j0 & 3);
+    uint32_t wv[kStreamT + 4];
+    if (bc == carry_cb) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wv[e] = carry[e];
+    } else {
+      const uint4 o = philox4x32_10(make_uint4(bc, 0u, sub, 0u), kk);
+      wv[0] = o.x;
+      wv[1] = o.y;
+      wv[2] = o.z;
+      wv[3] = o.w;
+    }
+#pragma unroll
+    for (int bq = 1; bq <= kStreamT / 4; ++bq) {
+      const uint4 o = philox4x32_10(make_uint4(bc + bq, 0u, sub, 0u), kk);
+      wv[4 * bq + 0] = o.x;
+      wv[4 * bq + 1] = o.y;
+      wv[4 * bq + 2] = o.z;
+      wv[4 * bq + 3] = o.w;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) carry[e] = wv[kStreamT + e];
+    carry_cb = bc + kStreamT / 4;
+    // draw t = word off + t of the window (bit-select masks on the offset, as k_bias_hub)
+    const uint32_t m2 = (off & 2) ? ~0u : 0u, m1 = (off & 1) ? ~0u : 0u;
+    float u[kStreamT];
+    uint32_t m = 0;  // bit t: edge i0 + 32 t passed the cheap bound
+#pragma unroll
+    for (int t = 0; t < kStreamT; ++t) {
+      const uint32_t w0 = bitsel(m2, wv[t + 2], wv[t]), w1 = bitsel(m2, wv[t + 3], wv[t + 1]);
+      u[t] = curand_uniform_from(bitsel(m1, w1, w0));
+      const bool valid = whole | (i0 + 32u * t < deg);
+      m |= (uint32_t)(valid & ares_may_pass_s(u[t], p[t], thr_s)) << t;
+    }
+    // the few that pass the bound go to the row's list as (u, edge); the merge computes their
+    // exact keys (keeping the fixed-operation key out of this loop saves registers)
+    while (half_ballot(m != 0)) {
+      const bool has = m != 0;
+      const int t = has ? __builtin_ctz(m) : 0;
+      m &= m - 1;
+      float ut = u[0];
+#pragma unroll
+      for (int e = 1; e < kStreamT; ++e) ut = t == e ? u[e] : ut;
+      const uint32_t b = half_ballot(has);
+      const int lead = __builtin_ctz(b);
+      int32_t old = 0;
+      if (l == lead) old = atomicAdd(a.cand.cnt + h, (int32_t)__builtin_popcount(b));
+      old = __shfl(old, lead, 32);
+      if (has) {
+        const int32_t pos = old + (int32_t)__builtin_popcount(b & ((1u << l) - 1u));
+        if (pos < cap) {
+          a.cand.key[(size_t)cb + pos] = ut;
+          a.cand.idx[(size_t)cb + pos] = (int32_t)(i0 + 32u * t);
+        }
+      }
+    }
+  }
+}
+
+// Emits each hub row's k picks from its candidate list (or recomputes the row when the list
+// overflowed).  Lists of at most 64: one half-wave per row.  Longer lists and recomputed rows: one workgroup per row, 8 half-waves
+// over interleaved 32-entry batches (or contiguous step ranges), merged in LDS.
+// Candidate e of a streamed row: its exact key from (u, edge) and the row's probabilities.
+__device__ __forceinline__ void stream_cand(const BiasHubArgs &a, global_ptr<float> pr, int64_t cb,
+                                            int32_t n, int32_t e, float &key, int32_t &idx) {
+  const bool v = e < n;
+  idx = v ? a.cand.idx[cb + e] : INT32_MAX;
+  key = v ? ares_key(a.cand.key[cb + e], pr[idx]) : -__builtin_inff();
+}
+
+__device__ __forceinline__ void stream_merge_block(const BiasHubArgs &a, int64_t blk,
+                                                   int64_t nblk) {
+  __shared__ float s_key[8][32];
+  __shared__ int32_t s_idx[8][32];
+  const int64_t S = a.Sc.get();
+  const int64_t G = (S + 15) / 16;
+  const int64_t H = (int64_t)((uint64_t)*a.hub.count >> kHubShift);
+  const int64_t k = a.k;
+  const int l = threadIdx.x & 31, g = threadIdx.x >> 5;
+  for (int64_t h = blk * 8 + g; h < H; h += nblk * 8) {
+    const int32_t n = a.cand.cnt[h], cap = a.cand.cap[h];
+    if (n > cap) continue;
+    if (n > 64) continue;
+    const int64_t cb = a.cand.base[h];
+    const global_ptr<float> pr = as_global(reinterpret_cast<const float *>(a.hub.aux[h]));
+    HalfTopK top;
+    for (int32_t b0 = 0; b0 < n; b0 += 32) {
+      float key;
+      int32_t idx;
+      stream_cand(a, pr, cb, n, b0 + l, key, idx);
+      top.push(key, idx, b0 + l < n, k, l);
+    }
+    merge_emit(a, S, h, top.bi, k, l);
+  }
+  for (int64_t h = blk; h < H; h += nblk) {
+    const int32_t n = a.cand.cnt[h], cap = a.cand.cap[h];
+    const bool recompute = n > cap;
+    if (!recompute && n <= 64) continue;
+    HalfTopK top;
+    if (recompute) {
+      const HubRowCtx c = hub_row_ctx(a, h, G, l);
+      const int64_t ns = (c.deg + 31) / 32;
+      bias_run(c, ns * g / 8, ns * (g + 1) / 8, k, l, top);
+    } else {
+      const int64_t cb = a.cand.base[h];
+      const global_ptr<float> pr = as_global(reinterpret_cast<const float *>(a.hub.aux[h]));
+      for (int32_t b0 = 32 * g; b0 < n; b0 += 256) {
+        float key;
+        int32_t idx;
+        stream_cand(a, pr, cb, n, b0 + l, key, idx);
+        top.push(key, idx, b0 + l < n, k, l);
+      }
+    }
+    tree_merge8(top, k, g, l, s_key, s_idx);
+    if (g == 0) merge_emit(a, S, h, s_idx[0][l], k, l);
+    __syncthreads();
+  }
 }
 
 // The biased hop's non-hub rows (workgroups [0, row_blocks)) and its hub-row merge (the rest) in
@@ -1296,6 +1807,8 @@ __global__ __launch_bounds__(kTileRows) void k_bias_rows_merge(
   if ((int64_t)blockIdx.x < row_blocks)
     sample_bias_block<false>(a.src, a.Sc, a.k, a.seed, a.rowinfo, a.tpre, a.boff, tpre2, tboff,
                              nullptr, a.rowpos, a.col, a.table, a.hub.hubid, blockIdx.x);
+  else if (a.cand.cnt)
+    stream_merge_block(a, (int64_t)blockIdx.x - row_blocks, merge_blocks);
   else
     bias_merge_block(a, (int64_t)blockIdx.x - row_blocks, merge_blocks);
 }
@@ -1338,10 +1851,47 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   int32_t *tpre = ws.tpre.as<int32_t>();
   int32_t *tpre2 = tpre + S;
   if (use_hubs) ws.hubslot.ensure(sizeof(int32_t) * (size_t)(S * k));
+  // Biased hubs: the streaming scheme (default) or the chunked one (DGS_BIAS_STREAM=0).
+  const bool stream = bias_hubs && bias_stream_on();
+  const int64_t nworkers =
+      (int64_t)(stream ? bias_stream_blocks() : bias_hub_blocks()) * (kTileRows / 32);
+  BiasCand cand{};
+  if (bias_hubs) {
+    // chunked: per-(worker + row) partial lists; streaming: per-row candidate lists.  Every
+    // streamed row's list fits the room below when the graph's edge count is known (the hop's
+    // rows are distinct: their degrees sum to at most E); otherwise rows past it are recomputed.
+    const int64_t slots = nworkers + S;
+    const size_t chunked = (sizeof(float) + sizeof(int32_t)) * (size_t)(slots * k) +
+                           sizeof(int32_t) * (size_t)(slots + 2 * S);
+    int64_t limit = 0;
+    size_t streaming = 0;
+    if (stream) {
+      // rows of one hop are distinct, so their chunks number at most E / chunk + S
+      const int64_t chunks =
+          src.num_edges > 0 ? src.num_edges / kStreamChunk + S : (int64_t(1) << 24);
+      limit = bias_room_start(S, chunks, k);
+      if (limit > INT32_MAX) limit = INT32_MAX;  // 32-bit list offsets (rows past it: recomputed)
+      streaming = sizeof(int64_t) * (size_t)S + 2 * sizeof(int32_t) * (size_t)S +
+                  (sizeof(float) + sizeof(int32_t)) * (size_t)limit;
+    }
+    ws.cand.ensure(chunked > streaming ? chunked : streaming);
+    if (stream) {
+      cand.base = ws.cand.as<int64_t>();
+      cand.cnt = reinterpret_cast<int32_t *>(cand.base + S);
+      cand.cap = cand.cnt + S;
+      cand.key = reinterpret_cast<float *>(cand.cap + S);
+      cand.idx = reinterpret_cast<int32_t *>(cand.key + limit);
+      cand.limit = limit;
+      // test hook, read per hop: DGS_BIAS_TEST_CAP=n limits a streamed row's list to n entries
+      // (n < k forces the exact recomputation of every streamed row)
+      const char *e = getenv("DGS_BIAS_TEST_CAP");
+      cand.cap_max = e ? atoll(e) : INT64_MAX;
+    }
+  }
   const PrepArgs pa{src, seeds, Sc, k, (int)replace,
                     use_hubs ? 1 : (bias_hubs ? 2 : 0),
                     (int)bias_replace, rowinfo, tpre, tpre2, bsum, tsum, hub,
-                    ws.hubslot.as<int32_t>(), table, next_count};
+                    ws.hubslot.as<int32_t>(), table, next_count, cand};
   if (tail)
     hipLaunchKernelGGL(k_prep_tail, dim3((unsigned)(tail->nblk + nb)), dim3(kTileRows), 0, st, pa,
                        *tail);
@@ -1382,20 +1932,25 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     DGS_CHECK(k <= 32, "biased sampling supports num_picks <= 32 (rowwise_sampling_bias.cu:73)");
     float *cdf = nullptr;
     const dim3 grid((unsigned)ceil_div(S, kBiasRowsPerBlock));
-    const int64_t nworkers = (int64_t)bias_hub_blocks() * (kTileRows / 32);
     BiasHubArgs ba{};
     if (bias_hubs) {
       const int64_t slots = nworkers + S;
-      ws.cand.ensure((sizeof(float) + sizeof(int32_t)) * (size_t)(slots * k) +
-                     sizeof(int32_t) * (size_t)(slots + 2 * S));
       float *ckey = ws.cand.as<float>();
       int32_t *cidx = reinterpret_cast<int32_t *>(ckey + slots * k);
       int32_t *ccnt = cidx + slots * k;
       int32_t *wfirst = ccnt + slots;
       ba = BiasHubArgs{src, Sc, k, launch_seed, rowinfo, tpre, boff, hub, ckey, cidx, ccnt,
-                       wfirst, wfirst + S, nworkers, rowpos, col, table};
-      hipLaunchKernelGGL(k_bias_hub, dim3(bias_hub_blocks()), dim3(kTileRows), 0, st, ba,
-                         (const int64_t *)bsum, boff, d_nnz);
+                       wfirst, wfirst + S, nworkers, rowpos, col, table, cand};
+      if (stream) {
+        hipLaunchKernelGGL(k_bias_boot, dim3((unsigned)std::min<int64_t>(S, 4096)),
+                           dim3(kTileRows), 0, st, ba);
+        DGS_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_bias_stream, dim3(bias_stream_blocks()), dim3(kTileRows), 0, st, ba,
+                           (const int64_t *)bsum, boff, d_nnz);
+      } else {
+        hipLaunchKernelGGL(k_bias_hub, dim3(bias_hub_blocks()), dim3(kTileRows), 0, st, ba,
+                           (const int64_t *)bsum, boff, d_nnz);
+      }
       DGS_LAUNCH_CHECK();
     }
     if (replace) {

@@ -164,6 +164,7 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
   src_.indices_base.p[kLocHost] = h_indices_.dev;
   src_.probs.p[kLocHost] = bias_ ? h_probs_.dev : nullptr;
   src_.num_nodes = num_nodes;
+  src_.num_edges = num_edges;
 }
 
 Sampler::~Sampler() {

@@ -114,6 +114,49 @@ def test_sample_neighbors_bias(dgs, k, replace):
     assert np.array_equal(col.cpu().numpy(), ec)
 
 
+def _bias_hub_graph(seed):
+    """Biased hub rows of every class of the streaming scheme (csrc/sample.hip): rows the boot
+    kernel solves outright (2048 < deg <= 8192), streamed rows (deg > 8192) up to 250K edges,
+    a streamed row with all-zero weights (no finite sample threshold) and one with only three
+    positive weights, plus ordinary rows."""
+    rng = np.random.default_rng(seed)
+    degs = rng.integers(0, 60, 300)
+    hubs = [2049, 3000, 5000, 8192, 8193, 9000, 20000, 30000, 70000, 250000]
+    degs[:len(hubs)] = hubs
+    indptr = np.concatenate([[0], np.cumsum(degs)]).astype(np.int64)
+    indices = rng.integers(0, degs.size, int(indptr[-1])).astype(np.int64)
+    probs = (rng.random(indices.size) + 0.01).astype(np.float32)
+    probs[::17] = 0.0
+    probs[indptr[6]:indptr[7]] = 0.0             # deg 20000: all zero
+    probs[indptr[7]:indptr[8]] = 0.0             # deg 30000: three positive weights
+    probs[indptr[7] + np.array([5, 17000, 29999])] = [0.5, 2.0, 1.0]
+    # deg 70000: weights rising along the row (a prefix sample would be unrepresentative)
+    probs[indptr[8]:indptr[9]] = np.linspace(0.01, 50.0, 70000, dtype=np.float32)
+    return indptr, indices, probs
+
+
+@pytest.mark.parametrize("cap", [None, "0", "40"])
+@pytest.mark.parametrize("k", [1, 5, 15, 32])
+def test_bias_hub_rows_streaming(dgs, k, cap, monkeypatch):
+    """Every class of biased hub row bit-exact against the oracle; DGS_BIAS_TEST_CAP squeezes the
+    streamed rows' candidate lists so they overflow and are recomputed exactly."""
+    if cap is not None:
+        monkeypatch.setenv("DGS_BIAS_TEST_CAP", cap)
+    indptr, indices, probs = _bias_hub_graph(3 + k)
+    n = indptr.size - 1
+    rng = np.random.default_rng(k)
+    seeds = np.concatenate([np.arange(10), rng.integers(0, n, 150), np.arange(10)])  # repeats
+    for s in (1, 2):
+        dgs.ops._CAPI_set_random_seed(900 + 10 * k + s)
+        ls = O.launch_seeds(900 + 10 * k + s, 1)[0]
+        row, col = dgs.ops._CAPI_cuda_sample_neighbors_bias(_cuda(seeds), _cuda(indptr),
+                                                            _cuda(indices), _cuda(probs), k,
+                                                            False)
+        er, ec = O.sample_bias(seeds, indptr, indices, probs, k, False, ls)
+        assert np.array_equal(row.cpu().numpy(), er)
+        assert np.array_equal(col.cpu().numpy(), ec)
+
+
 def test_sample_golden_vectors(dgs):
     z = _gold()
     seeds, indptr, indices, probs = z["seeds"], z["indptr"], z["indices"], z["probs"]

@@ -25,9 +25,14 @@ first="${libs[0]}"; last="${libs[${#libs[@]}-1]}"
 files=()
 for lib in "$first" "$last"; do
   n=$(echo "$lib" | tr '/,=' '___')
-  DGS_AMD_LIB="$R/${lib%%,*}" timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-    -d $O/k_$n -- python3 bench.py --no-cpu-baseline --bias --depth 1 --steps 200 --warmup 10 "$@" \
-    > $O/k_$n.log 2>&1 || { tail -20 $O/k_$n.log; exit 1; }
+  (
+    IFS=, read -ra parts <<< "$lib"
+    export DGS_AMD_LIB="$R/${parts[0]}"
+    for kv in "${parts[@]:1}"; do export "$kv"; done
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d $O/k_$n -- python3 bench.py --no-cpu-baseline --bias --depth 1 --steps 200 --warmup 10 "$@" \
+      > $O/k_$n.log 2>&1
+  ) || { tail -20 $O/k_$n.log; exit 1; }
   files+=("$(find $O/k_$n -name "*kernel_stats.csv" | head -1)")
 done
 python3 tools/prof_summary.py --compare "${files[@]}" > $O/kernels.txt; head -14 $O/kernels.txt
