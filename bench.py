@@ -544,6 +544,13 @@ def main():
             "frac": side["iso_gbps"] / HBM_PEAK_GBPS,
             "avg_launch_ms": side["iso_ms"],
         },
+        # SURVEY 8(d)'s gather micro-bench (2^20 random nids, the same feature server)
+        "roofline_microbench": {
+            "rows": 1 << 20, "nids": "randint(0, N, 2^20), generator seed 3",
+            "achieved": side["mb_gbps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": side["mb_gbps"] / HBM_PEAK_GBPS,
+            "avg_launch_ms": side["mb_ms"],
+        },
         "cpu_baseline": cpu,
     }
     if world > 1 and mode != "replicated":
@@ -620,6 +627,23 @@ def side_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, cache
     torch.cuda.synchronize()
     iso = dgs.ops.profile_read()
     dgs.ops.profile_enable(False)
+    # SURVEY 8(d) gather micro-bench: n = 2^20 uniform random nids (generator seed 3) through the
+    # same feature server, 5 launches after a warm-up, kernel time from the same stamps
+    dev = labels_dev.device
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(3)
+    mb_nids = torch.randint(0, cached_mask.numel(), (1 << 20,), generator=gen, device=dev)
+    server._CAPI_get_feature(mb_nids)
+    torch.cuda.synchronize()
+    dgs.ops.profile_enable(dgs.ops.PROFILE_GATHER)
+    for _ in range(5):
+        server._CAPI_get_feature(mb_nids)
+    torch.cuda.synchronize()
+    mb = dgs.ops.profile_read()
+    dgs.ops.profile_enable(False)
+    mb_launches = max(mb["gather_launches"], 1)
+    mb_ms = mb["gather_ms"] / mb_launches
+    del mb_nids
     # SURVEY 8(d) metric (2): algorithmic bytes / wall time of one synchronous _CAPI_get_feature
     # call (host launch + kernel + synchronisation), median over the side pass
     g_rates = []
@@ -640,6 +664,8 @@ def side_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, cache
                      if iso["gather_ms"] > 0 else 0.0),
         "iso_ms": iso["gather_ms"] / max(iso["gather_launches"], 1),
         "call_gbps": float(np.median(g_rates)) if g_rates else 0.0,
+        "mb_ms": mb_ms,
+        "mb_gbps": (1 << 20) * per_row / (mb_ms * 1e-3) / 1e9 if mb_ms > 0 else 0.0,
     }
 
 

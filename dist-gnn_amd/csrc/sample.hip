@@ -30,10 +30,10 @@ constexpr int kGroup = 16;       // lanes per row in the uniform kernel
 constexpr int kRowsPerBlock = kTileRows / kGroup;  // rows per uniform-sampling workgroup
 constexpr int kHubT = 128;       // reservoir tail length above which a row goes to the hub kernel
 #ifndef DGS_BIAS_HUB_T
-#define DGS_BIAS_HUB_T 2048
+#define DGS_BIAS_HUB_T 1024
 #endif
-// biased rows above this degree are split across half-waves (round 2: 2048 instead of 1024,
-// +2.8 % at B = 1024, +3.7 % at 8192, +-0 papers-scale; 256 / 512 / 4096 / 8192 worse)
+// biased rows above this degree go to the hub kernels (round 3, streaming scheme: 1024 and 2048
+// equal pipelined, 1024 has the shorter single call; 4096 -13 %.  Round 2's chunked scheme: 2048)
 constexpr int kBiasHubT = DGS_BIAS_HUB_T;
 #ifndef DGS_BIAS_CHUNK
 #define DGS_BIAS_CHUNK 256
@@ -74,7 +74,7 @@ bool bias_stream_on() {
   }();
   return on;
 }
-constexpr int kBiasStreamBlocks = 1024;
+constexpr int kBiasStreamBlocks = 768;  // round 3 A/B: 512-768 best, 1024 -1.5 %, 1536 -9 %
 // Workgroups of the streaming kernel; DGS_BIAS_STREAM_BLOCKS overrides.
 int bias_stream_blocks() {
   static const int n = [] {
@@ -186,8 +186,10 @@ __device__ __forceinline__ float key_from_order(int32_t m) {
 #endif
 constexpr int64_t kBiasSampleSteps = DGS_BIAS_SAMPLE_STEPS;
 // Steps per streamed chunk (a chunk = 32 kStreamT edges; one new Philox block per 4 steps).
+// Round 3 A/B: 8 steps +3 % over 4 (90 against 75 VGPRs, but half the row switches and
+// threshold loads per edge); 12 equal, 16 -4 %.
 #ifndef DGS_BIAS_STREAM_T
-#define DGS_BIAS_STREAM_T 4
+#define DGS_BIAS_STREAM_T 8
 #endif
 constexpr int kStreamT = DGS_BIAS_STREAM_T;
 constexpr int kStreamChunk = 32 * kStreamT;

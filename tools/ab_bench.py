@@ -42,7 +42,7 @@ def main():
         for lib in libs:
             cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline"] + extra
             out = subprocess.run(cmd, env=variant_env(lib), capture_output=True, text=True,
-                                 timeout=300)
+                                 timeout=int(os.environ.get("AB_TIMEOUT", "300")))
             if out.returncode != 0:
                 sys.stderr.write(out.stderr[-2000:])
                 sys.exit(out.returncode)
