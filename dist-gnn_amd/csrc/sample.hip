@@ -35,12 +35,6 @@ constexpr int kHubT = 128;       // reservoir tail length above which a row goes
 // biased rows above this degree go to the hub kernels (round 3, streaming scheme: 1024 and 2048
 // equal pipelined, 1024 has the shorter single call; 4096 -13 %.  Round 2's chunked scheme: 2048)
 constexpr int kBiasHubT = DGS_BIAS_HUB_T;
-#ifndef DGS_BIAS_CHUNK
-#define DGS_BIAS_CHUNK 256
-#endif
-constexpr int kBiasChunk = DGS_BIAS_CHUNK;  // edges per biased hub chunk (32 lanes x 8 draws)
-constexpr int kBiasHubBlocks = 768;  // workgroups of the biased hub kernel (8 half-waves each): 3 of
-                                      // its 4 resident waves per SIMD, room for the other batches
 constexpr int kHubBlocks = 1536; // workgroups of the hub kernel: 6 of 8 waves per SIMD, so the
                                  // other batches in flight (feature gather) find free slots
 constexpr int kMaxPicksLds = 512;
@@ -56,24 +50,6 @@ int hub_blocks() {
   return n;
 }
 
-// Workgroups of the biased hub kernel; DGS_BIAS_HUB_BLOCKS overrides (occupancy experiments).
-int bias_hub_blocks() {
-  static const int n = [] {
-    const char *e = getenv("DGS_BIAS_HUB_BLOCKS");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : kBiasHubBlocks;
-  }();
-  return n;
-}
-
-// Biased hub rows: streaming scheme (default) or the chunked one (DGS_BIAS_STREAM=0, A/B).
-bool bias_stream_on() {
-  static const bool on = [] {
-    const char *e = getenv("DGS_BIAS_STREAM");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
 constexpr int kBiasStreamBlocks = 768;  // round 3 A/B: 512-768 best, 1024 -1.5 %, 1536 -9 %
 // Workgroups of the streaming kernel; DGS_BIAS_STREAM_BLOCKS overrides.
 int bias_stream_blocks() {
@@ -215,7 +191,7 @@ struct BiasCand {
   float *key;
   int32_t *idx;
   int64_t limit;                // entries of key / idx
-  int64_t cap_max;              // test hook (DGS_BIAS_TEST_CAP): caps every streamed row's room
+  int64_t cap_max;              // test hook (DGS_BIAS_TEST_CAP): caps every row's room
 };
 
 // ------------------------------------------------------------------------------------
@@ -238,7 +214,7 @@ struct PrepArgs {
   int32_t *hubslot;
   Table table;
   int64_t *next_hub_count;
-  BiasCand cand;  // biased hubs, streaming scheme (cand.cnt == nullptr: chunked scheme)
+  BiasCand cand;  // biased hubs: per-row candidate lists
 };
 
 __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
@@ -266,12 +242,11 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
     if (a.use_hubs) {
       int64_t h = -1;
       // 1: uniform hubs (reservoir tail > kHubT, 512-edge chunks); 2: biased hubs (degree >
-      // kBiasHubT, kBiasChunk-edge chunks)
+      // kBiasHubT, kStreamChunk-edge chunks)
       const bool is_hub = a.use_hubs == 1 ? deg - k > kHubT : deg > kBiasHubT;
       if (is_hub) {
         const uint64_t nch = a.use_hubs == 1 ? (uint64_t)(deg - k + 511) / 512
-                             : a.cand.cnt   ? (uint64_t)(deg + kStreamChunk - 1) / kStreamChunk
-                                            : (uint64_t)(deg + kBiasChunk - 1) / kBiasChunk;
+                                             : (uint64_t)(deg + kStreamChunk - 1) / kStreamChunk;
         const uint64_t old = atomicAdd((unsigned long long *)a.hub.count,
                                        (unsigned long long)((uint64_t(1) << kHubShift) | nch));
         h = (int64_t)(old >> kHubShift);
@@ -283,7 +258,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
         } else {
           a.hub.thr[h] = key_order(-__builtin_inff());
           a.hub.aux[h] = (int64_t)row_probs(a.src, ri);
-          if (a.cand.cnt) {
+          {  // the row's candidate room, addressed from its chunk offset
             const int64_t c0 = (int64_t)(old & kHubChunkMask);
             const int64_t b = bias_room_start(h, c0, k);
             int64_t cap = bias_room_start(h + 1, c0 + (int64_t)nch, k) - b;
@@ -813,7 +788,7 @@ __device__ __forceinline__ void sample_bias_block(
         }
         return;
       }
-      if (hubid && hubid[r] >= 0) return;  // split across half-waves: k_bias_hub / _merge
+      if (hubid && hubid[r] >= 0) return;  // a hub row: k_bias_boot / _stream / the merge
       HalfTopK top;
       // Step s of this lane (edge i = 32 s + l) uses draw j + s.  Steps go in groups of 4
       // over a window of two Philox blocks, one new block per group for every lane alike (the
@@ -956,10 +931,8 @@ __global__ __launch_bounds__(kTileRows) void k_sample_bias(
 // ------------------------------------------------------------------------------------
 // Biased hub rows (A-Res without replacement, degree > kBiasHubT).  Edge i of a row draws
 // curand number j = c_l + i / 32 of subsequence 32w + l (l = i % 32; c_l = draws lane l made on
-// the chain's earlier rows), so any half-wave can evaluate any edge's key.  Half-wave workers
-// take contiguous ranges of kBiasChunk-edge chunks over the hub list, keep a running top-k per
-// row and flush it to slot (worker + hub) -- unique, since the (worker, hub) pairs a static
-// partition visits form a staircase -- and k_bias_hub_merge reduces each row's slots.
+// the chain's earlier rows), so any half-wave can evaluate any edge's key (see k_bias_boot /
+// k_bias_stream below).
 struct BiasHubArgs {
   RowSrc src;
   Count Sc;
@@ -969,16 +942,11 @@ struct BiasHubArgs {
   const int32_t *tpre;
   const int64_t *boff;
   HubView hub;
-  float *ckey;
-  int32_t *cidx;
-  int32_t *ccnt;
-  int32_t *wfirst;  // per hub row: workers holding its first / last chunk
-  int32_t *wlast;
-  int64_t nworkers;
+  int64_t nworkers;  // half-wave workers of k_bias_stream
   int64_t *rowpos;
   int64_t *col;
   Table table;
-  BiasCand cand;  // streaming scheme (cand.cnt != nullptr)
+  BiasCand cand;
 };
 
 // draws lane l made on the earlier rows of row r's (block, warp) chain (no replacement)
@@ -998,291 +966,10 @@ __device__ __forceinline__ int64_t bias_worker_c0(int64_t total, int64_t w, int6
   return total * w / nw;
 }
 
-// Workers actually used: at least 2 chunks each (parallelism wins over longer row segments:
-// measured 4 and 8 chunks slower); both kernels derive it from the same device-side total.
+// Workers actually used: at least 2 chunks each (parallelism wins over longer row segments).
 __device__ __forceinline__ int64_t bias_workers(int64_t total, int64_t max_workers) {
   const int64_t w = total / 2;
   return w < 1 ? 1 : (w > max_workers ? max_workers : w);
-}
-
-#ifndef DGS_BIAS_HUB_WAVES
-#define DGS_BIAS_HUB_WAVES 1
-#endif
-__global__ __launch_bounds__(kTileRows, DGS_BIAS_HUB_WAVES) void k_bias_hub(BiasHubArgs a,
-                                                                           const int64_t *bsum,
-                                                                           int64_t *boff,
-                                                                           int64_t *d_nnz) {
-  if (blockIdx.x == 0) {
-    // the hop's tile-offset scan (k_scan_hop's job), which k_sample_bias after it reads
-    __shared__ int64_t lds[kTileRows / 64];
-    const int64_t nb = (a.Sc.get() + kTileRows - 1) / kTileRows;
-    const int64_t tot = block_scan_range<kTileRows, 8>(bsum, nb, boff, lds);
-    if (threadIdx.x == 0) {
-      boff[nb] = tot;
-      *d_nnz = tot;
-    }
-  }
-  const int64_t S = a.Sc.get();
-  const int64_t G = (S + 15) / 16;
-  const uint64_t packed = (uint64_t)*a.hub.count;
-  const int64_t H = (int64_t)(packed >> kHubShift);
-  if (H == 0) return;
-  const int64_t total = (int64_t)(packed & kHubChunkMask);
-  const int l = threadIdx.x & 31;
-  const int64_t wk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 5;
-  const int64_t nw = bias_workers(total, a.nworkers);
-  if (wk >= nw) return;
-  const int64_t c0 = bias_worker_c0(total, wk, nw);
-  const int64_t c1 = bias_worker_c0(total, wk + 1, nw);
-  if (c0 >= c1) return;
-  const int64_t k = a.k;
-  int64_t h = group_search<32>(a.hub.cptr, H, c0);  // largest h with cptr[h] <= c0
-  int64_t hstart = 0, hnext = 0, deg = 0, jb = 0;
-  global_ptr<float> pr = nullptr;
-  int32_t published = key_order(-__builtin_inff());
-  uint2 kk;
-  uint32_t sub = 0;
-  HalfTopK top;
-  auto load_row = [&](int64_t hh) {
-    hstart = a.hub.cptr[hh];
-    hnext = hh + 1 < H ? a.hub.cptr[hh + 1] : total;
-    const int64_t r = a.hub.row[hh];
-    deg = ri_deg(a.rowinfo[r]);
-    pr = as_global(reinterpret_cast<const float *>(a.hub.aux[hh]));
-    const uint64_t key = a.seed * (uint64_t)G + (uint64_t)(r / 16);
-    kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
-    sub = (uint32_t)(32 * ((r % 16) & 3) + l);
-    jb = chain_draws(a.rowinfo, r, k, l);
-    top = HalfTopK();
-    published = key_order(-__builtin_inff());
-  };
-  // Candidates wait in a per-half-wave LDS buffer and are merged into the list 32 at a time:
-  // each insertion costs cross-lane shuffles whose latency the few co-resident waves of this
-  // register-heavy kernel can not hide, so they are paid once per 32 candidates.  The list's
-  // k-th key (the filter) then trails by at most one buffer; anything it lets through is
-  // dropped exactly at the merge.
-  __shared__ float s_ck[kTileRows / 32][64];
-  __shared__ int32_t s_ci[kTileRows / 32][64];
-  const int hw = threadIdx.x >> 5;
-  int ncand = 0;  // buffered candidates of this half-wave (the same on its 32 lanes)
-  auto merge = [&]() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    while (ncand > 0) {
-      const int n = ncand < 32 ? ncand : 32;
-      const bool v = l < n;
-      const float ck = v ? s_ck[hw][ncand - n + l] : -__builtin_inff();
-      const int32_t ci = v ? s_ci[hw][ncand - n + l] : INT32_MAX;
-      top.push(ck, ci, v, k, l);
-      ncand -= n;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-  auto flush = [&](int64_t hh) {
-    merge();
-    const int64_t slot = wk + hh;
-    if (l < top.cnt) {
-      a.ckey[slot * k + l] = top.bk;
-      a.cidx[slot * k + l] = top.bi;
-    }
-    if (l == 0) a.ccnt[slot] = top.cnt;
-  };
-  load_row(h);
-  constexpr int kT = kBiasChunk / 32;
-  const int32_t published_none = key_order(-__builtin_inff());
-  // the last Philox block of a chunk is the first of the row's next chunk (draws run on)
-  uint32_t carry[4] = {0u, 0u, 0u, 0u};
-  int64_t carry_cb = -1;
-  for (int64_t c = c0; c < c1; ++c) {
-    while (c >= hnext) {
-      flush(h);
-      ++h;
-      load_row(h);
-      carry_cb = -1;
-    }
-    const int64_t q = c - hstart;
-    if (l == 0 && c == hstart) a.wfirst[h] = (int32_t)wk;
-    if (l == 0 && c == hnext - 1) a.wlast[h] = (int32_t)wk;
-    // Every worker's k-th key bounds the row's final k-th key from below, so the best one
-    // published so far filters this worker's edges too (stale reads only filter less).
-    // (Loading it and the probabilities one chunk ahead costs more registers than the latency
-    // it hides: 3 instead of 4 waves per SIMD, -20 %.)
-    const int32_t shared_ord =
-        (int32_t)__hip_atomic_load(a.hub.thr + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int64_t i0 = q * kBiasChunk + l;
-    const bool whole = q * kBiasChunk + kBiasChunk <= deg;  // no edge of the chunk past the row
-    float p[kT];
-    {
-      // row-local edge indices fit 32 bits (deg < 2^31): 32-bit offset arithmetic, one
-      // 64-bit address add per load (the 64-bit form took 14 more VGPRs)
-      const uint32_t i32 = (uint32_t)i0, last = (uint32_t)(deg - 1);
-#pragma unroll
-      for (int t = 0; t < kT; ++t) {
-        const uint32_t i = i32 + 32u * t;
-        p[t] = pr[whole ? i : (i < last ? i : last)];
-      }
-    }
-    // this lane's kT draws j = jb + kT q + t lie in kT / 4 + 1 consecutive Philox blocks
-    // (uniform control flow -- lanes' chain offsets differ, a lazy per-lane refill would diverge
-    // into a Philox per step); select draw t as word off + t.  The first block was the previous
-    // chunk's last whenever the worker stays in the row, so kT / 4 are computed.
-    const int64_t j0 = jb + q * kT;
-    const int64_t cb = j0 >> 2;
-    const int off = (int)(j0 & 3);
-    uint32_t wv[4 * (kT / 4 + 1)];
-    if (cb == carry_cb) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) wv[e] = carry[e];
-    } else {
-      const uint4 o = philox4x32_10(make_uint4((uint32_t)cb, (uint32_t)((uint64_t)cb >> 32), sub, 0u), kk);
-      wv[0] = o.x;
-      wv[1] = o.y;
-      wv[2] = o.z;
-      wv[3] = o.w;
-    }
-#pragma unroll
-    for (int bq = 1; bq < kT / 4 + 1; ++bq) {
-      const uint64_t cq = (uint64_t)(cb + bq);
-      const uint4 o = philox4x32_10(make_uint4((uint32_t)cq, (uint32_t)(cq >> 32), sub, 0u), kk);
-      wv[4 * bq + 0] = o.x;
-      wv[4 * bq + 1] = o.y;
-      wv[4 * bq + 2] = o.z;
-      wv[4 * bq + 3] = o.w;
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) carry[e] = wv[4 * (kT / 4) + e];
-    carry_cb = cb + kT / 4;
-    // draw t = word off + t, selected in two steps (off & 2, then off & 1) with bit-select
-    // masks (a select on the offset bit would be folded into a dynamically indexed array)
-    const uint32_t m2 = (off & 2) ? ~0u : 0u, m1 = (off & 1) ? ~0u : 0u;
-    uint32_t w2[kT + 1];
-#pragma unroll
-    for (int e = 0; e < kT + 1; ++e) w2[e] = bitsel(m2, wv[e + 2], wv[e]);
-    // every draw of the chunk is computed before the first probability is used, so the
-    // probability loads' latency hides under all of the chunk's Philox work (the scheduler
-    // otherwise starts the filter after a third of it; with the 32-bit indices: +3.8 %)
-#pragma unroll
-    for (int e = 0; e < kT + 1; ++e) asm volatile("" ::"v"(w2[e]));
-    // The chunk's filter threshold, fixed for its 16 steps: this worker's k-th key once its list
-    // is full, or the best k-th any worker of the row has published -- both lower bounds of the
-    // row's final k-th key, so an edge the cheap test rejects can not be among the row's picks.
-    bool filter = top.filtering(k) || shared_ord != published_none;
-    float thr_s = slack_thr(key_from_order(
-        top.filtering(k) ? max(key_order(top.thr_k), shared_ord) : shared_ord));
-    const uint32_t deg32 = (uint32_t)deg;
-    float u[kT];
-    uint32_t m = 0;  // bit t: edge i0 + 32 t is a candidate
-#pragma unroll
-    for (int t = 0; t < kT; ++t) {
-      u[t] = curand_uniform_from(bitsel(m1, w2[t + 1], w2[t]));
-      const bool valid = whole | ((uint32_t)i0 + 32u * t < deg32);
-      m |= (uint32_t)(valid & (!filter | ares_may_pass_s(u[t], p[t], thr_s))) << t;
-    }
-    // Candidates go into the top-k list in rounds of one per lane (each round one sorted
-    // merge, or one-by-one insertion when few lanes have one); the resulting list does not
-    // depend on the order.  Unfiltered (the worker's first steps in a row), the rest of the
-    // candidates are re-tested once the first round has filled the list.
-    while (half_ballot(m != 0)) {
-      const bool has = m != 0;
-      const int t = has ? __builtin_ctz(m) : 0;
-      m &= m - 1;
-      float ut = u[0], pt = p[0];
-#pragma unroll
-      for (int e = 1; e < kT; ++e) {
-        ut = t == e ? u[e] : ut;
-        pt = t == e ? p[e] : pt;
-      }
-      const float key = has ? ares_key(ut, pt) : -__builtin_inff();
-      const int32_t it = (int32_t)(i0 + 32 * t);
-      const bool keep = has && ares_better(key, it, top.thr_k, top.thr_i);
-      const uint32_t b = half_ballot(keep);
-      if (keep) {
-        const int pos = ncand + __builtin_popcount(b & ((1u << l) - 1u));
-        s_ck[hw][pos] = key;
-        s_ci[hw][pos] = it;
-      }
-      ncand += __builtin_popcount(b);
-      if (ncand >= 32) merge();
-      if (!filter && top.filtering(k)) {
-        filter = true;
-        thr_s = slack_thr(top.thr_k);
-        uint32_t keep = 0;
-#pragma unroll
-        for (int e = 0; e < kT; ++e)
-          keep |= (uint32_t)ares_may_pass_s(u[e], p[e], thr_s) << e;
-        m &= keep;
-      }
-    }
-    // publish this worker's k-th key when it improved on what it last published
-    if (top.filtering(k)) {
-      const int32_t mine = key_order(top.thr_k);
-      if (mine > published && mine > shared_ord) {
-        if (l == 0) atomicMax((long long *)(a.hub.thr + h), (long long)mine);
-        published = mine;
-      }
-    }
-  }
-  flush(h);
-}
-
-#ifndef DGS_MERGE_HALF_SLOTS
-#define DGS_MERGE_HALF_SLOTS 8
-#endif
-// Rows whose chunks went to at most this many workers are merged by one half-wave each (8 rows
-// per workgroup at once, no barrier); the others by a whole workgroup.
-constexpr int64_t kMergeHalfSlots = DGS_MERGE_HALF_SLOTS;
-
-// The worker slots of row h from w0 on (every `step`-th pair when per == 2) pushed into `top`.
-__device__ __forceinline__ void merge_slots(const BiasHubArgs &a, HalfTopK &top, int64_t h,
-                                            int64_t wf, int64_t wl, int64_t first, int64_t step,
-                                            int64_t total, int64_t nw, int64_t k, int l) {
-  // k <= 16: two workers' lists per batch (lanes 0-15 and 16-31), else one
-  const int per = k <= 16 ? 2 : 1;
-  const int part = per == 2 ? (l >> 4) : 0;
-  const int e = per == 2 ? (l & 15) : l;
-  // a worker's list is sorted (descending); the second list of a pair is read in reverse
-  // so the 32 lanes hold a bitonic sequence
-  const int er = part ? 15 - e : e;
-  // A batch's count and entries are loaded together (the entry address does not wait for the
-  // count: lanes past the count are masked afterwards), and the next batch's loads go out before
-  // the current batch is merged, so a long slot list pays about one load latency in all instead
-  // of two per batch (round 3).
-  const int erc = er < (int)k ? er : (int)k - 1;  // inside this slot's k entries
-  auto fetch = [&](int64_t w0, int &n, float &key_i, int32_t &i) {
-    const int64_t w = w0 + part;
-    const bool have =
-        w <= wl && bias_worker_c0(total, w, nw) != bias_worker_c0(total, w + 1, nw);
-    const int64_t slot = (have ? w : wf) + h;  // a valid slot either way
-    n = a.ccnt[slot];
-    key_i = a.ckey[slot * k + erc];
-    i = a.cidx[slot * k + erc];
-    if (!have) n = 0;
-  };
-  const int64_t stride = step * per;
-  int64_t w0 = wf + (int64_t)per * first;
-  if (w0 > wl) return;
-  int n;
-  float key_i;
-  int32_t i;
-  fetch(w0, n, key_i, i);
-  for (;;) {
-    const int64_t wn = w0 + stride;
-    int n2 = 0;
-    float key2 = -__builtin_inff();
-    int32_t i2 = INT32_MAX;
-    if (wn <= wl) fetch(wn, n2, key2, i2);
-    const bool valid = er < n;
-    top.push_bitonic(valid ? key_i : -__builtin_inff(), valid ? i : INT32_MAX, valid, k, l,
-                     per == 1);
-    if (wn > wl) break;
-    w0 = wn;
-    n = n2;
-    key_i = key2;
-    i = i2;
-  }
 }
 
 // Writes row h's k picks (lane l < k: the l-th best, index idx_l).
@@ -1299,76 +986,11 @@ __device__ __forceinline__ void merge_emit(const BiasHubArgs &a, int64_t S, int6
   }
 }
 
-// Reduces each hub row's worker slots to its k picks.  Rows with few slots: one half-wave per
-// row.  The others: one workgroup per row, whose 8 half-waves reduce interleaved subsets of the
-// slots before half-wave 0 merges the 8 partial lists and emits the picks.
-__device__ __forceinline__ void bias_merge_block(const BiasHubArgs &a, int64_t blk, int64_t nblk) {
-  __shared__ float s_key[8][32];
-  __shared__ int32_t s_idx[8][32];
-  const int64_t S = a.Sc.get();
-  const uint64_t packed = (uint64_t)*a.hub.count;
-  const int64_t H = (int64_t)(packed >> kHubShift);
-  const int64_t total = (int64_t)(packed & kHubChunkMask);
-  const int64_t nw = bias_workers(total, a.nworkers);
-  const int64_t k = a.k;
-  const int l = threadIdx.x & 31, g = threadIdx.x >> 5;
-  for (int64_t h = blk * 8 + g; h < H; h += nblk * 8) {
-    const int64_t wf = a.wfirst[h], wl = a.wlast[h];
-    if (wl - wf + 1 > kMergeHalfSlots) continue;
-    HalfTopK top;
-    merge_slots(a, top, h, wf, wl, 0, 1, total, nw, k, l);
-    merge_emit(a, S, h, l < k && top.bi != INT32_MAX ? top.bi : INT32_MAX, k, l);
-  }
-  for (int64_t h = blk; h < H; h += nblk) {
-    const int64_t wf = a.wfirst[h], wl = a.wlast[h];
-    if (wl - wf + 1 <= kMergeHalfSlots) continue;
-    HalfTopK top;
-    merge_slots(a, top, h, wf, wl, g, 8, total, nw, k, l);
-    // the 8 half-waves' lists (sorted, only the first k count: an entry past its own list's
-    // k-th can not be among the k best of the union) merged pairwise in a tree
-    const bool mine = l < k && top.bi != INT32_MAX;
-    s_key[g][l] = mine ? top.bk : -__builtin_inff();
-    s_idx[g][l] = mine ? top.bi : INT32_MAX;
-    __syncthreads();
-#pragma unroll
-    for (int step = 1; step < 8; step <<= 1) {
-      if ((g & (2 * step - 1)) == 0) {
-        float mk = s_key[g][l];
-        int32_t mi = s_idx[g][l];
-        const float ok = s_key[g + step][31 - l];
-        const int32_t oi = s_idx[g + step][31 - l];
-        if (ares_better(ok, oi, mk, mi)) {
-          mk = ok;
-          mi = oi;
-        }
-#pragma unroll
-        for (int stride = 16; stride > 0; stride >>= 1)
-          HalfTopK::cas(mk, mi, stride, (l & stride) == 0);
-        s_key[g][l] = mk;
-        s_idx[g][l] = mi;
-      }
-      __syncthreads();
-    }
-    if (g == 0) merge_emit(a, S, h, s_idx[0][l], k, l);
-    __syncthreads();
-  }
-}
-
-__device__ __forceinline__ void stream_merge_block(const BiasHubArgs &a, int64_t blk,
-                                                   int64_t nblk);
-__global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
-  latency_prio();
-  if (a.cand.cnt)
-    stream_merge_block(a, blockIdx.x, gridDim.x);
-  else
-    bias_merge_block(a, blockIdx.x, gridDim.x);
-}
-
 // ------------------------------------------------------------------------------------
-// Biased hub rows, streaming scheme (round 3).  The chunked scheme above keeps a running top-k
-// per half-wave worker: 112 VGPRs, 4 waves per SIMD, and its per-edge loop waits on probability
-// and threshold loads it can not hide (0.41 T edges/s against ~1 T for the same Philox +
-// filter work VALU-bound).  Here the work is split so the per-edge pass holds no top-k state:
+// Biased hub rows, streaming scheme (round 3).  Round 2's chunked scheme kept a running top-k per
+// half-wave worker: 112 VGPRs, 4 waves per SIMD, and its per-edge loop waited on probability and
+// threshold loads it could not hide (0.41 T edges/s against ~1 T for the same Philox + filter
+// work VALU-bound).  Here the work is split so the per-edge pass holds no top-k state:
 //   k_bias_boot    one workgroup per hub row: over a spread sample (8 runs of kBiasSampleSteps
 //                  steps, 4096 edges) each lane keeps the largest key_lower() (a provable
 //                  lower bound of the exact key, from the hardware log2); the k-th largest of
@@ -1381,8 +1003,8 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
 //   merge          (in k_bias_rows_merge) exact keys of each row's candidates and their top-k;
 //                  a row whose list overflowed (or whose sample had no finite k-th key) is
 //                  recomputed exactly.
-// Every edge's key comes from its reference coordinates, so the picks are those of the chunked
-// scheme (and of the oracle), bit for bit.
+// Every edge's key comes from its reference coordinates, so the picks are the oracle's, bit for
+// bit, however the work is split.
 
 struct HubRowCtx {
   int64_t r, deg;
@@ -1704,7 +1326,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
 #pragma unroll
     for (int e = 0; e < 4; ++e) carry[e] = wv[kStreamT + e];
     carry_cb = bc + kStreamT / 4;
-    // draw t = word off + t of the window (bit-select masks on the offset, as k_bias_hub)
+    // draw t = word off + t of the window, picked with bit-select masks on the offset
     const uint32_t m2 = (off & 2) ? ~0u : 0u, m1 = (off & 1) ? ~0u : 0u;
     float u[kStreamT];
     uint32_t m = 0;  // bit t: edge i0 + 32 t passed the cheap bound
@@ -1809,10 +1431,14 @@ __global__ __launch_bounds__(kTileRows) void k_bias_rows_merge(
   if ((int64_t)blockIdx.x < row_blocks)
     sample_bias_block<false>(a.src, a.Sc, a.k, a.seed, a.rowinfo, a.tpre, a.boff, tpre2, tboff,
                              nullptr, a.rowpos, a.col, a.table, a.hub.hubid, blockIdx.x);
-  else if (a.cand.cnt)
-    stream_merge_block(a, (int64_t)blockIdx.x - row_blocks, merge_blocks);
   else
-    bias_merge_block(a, (int64_t)blockIdx.x - row_blocks, merge_blocks);
+    stream_merge_block(a, (int64_t)blockIdx.x - row_blocks, merge_blocks);
+}
+
+// The hub-row merge alone (DGS_BIAS_SPLIT_MERGE=1: rows and merge as two launches, profiling).
+__global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
+  latency_prio();
+  stream_merge_block(a, blockIdx.x, gridDim.x);
 }
 
 }  // namespace
@@ -1853,42 +1479,28 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   int32_t *tpre = ws.tpre.as<int32_t>();
   int32_t *tpre2 = tpre + S;
   if (use_hubs) ws.hubslot.ensure(sizeof(int32_t) * (size_t)(S * k));
-  // Biased hubs: the streaming scheme (default) or the chunked one (DGS_BIAS_STREAM=0).
-  const bool stream = bias_hubs && bias_stream_on();
-  const int64_t nworkers =
-      (int64_t)(stream ? bias_stream_blocks() : bias_hub_blocks()) * (kTileRows / 32);
+  // Biased hubs: per-row candidate lists.  Every row's list fits the room below when the graph's
+  // edge count is known (a hop's rows are distinct: their chunks number at most E / chunk + S);
+  // otherwise rows past it are recomputed exactly.
+  const int64_t nworkers = (int64_t)bias_stream_blocks() * (kTileRows / 32);
   BiasCand cand{};
   if (bias_hubs) {
-    // chunked: per-(worker + row) partial lists; streaming: per-row candidate lists.  Every
-    // streamed row's list fits the room below when the graph's edge count is known (the hop's
-    // rows are distinct: their degrees sum to at most E); otherwise rows past it are recomputed.
-    const int64_t slots = nworkers + S;
-    const size_t chunked = (sizeof(float) + sizeof(int32_t)) * (size_t)(slots * k) +
-                           sizeof(int32_t) * (size_t)(slots + 2 * S);
-    int64_t limit = 0;
-    size_t streaming = 0;
-    if (stream) {
-      // rows of one hop are distinct, so their chunks number at most E / chunk + S
-      const int64_t chunks =
-          src.num_edges > 0 ? src.num_edges / kStreamChunk + S : (int64_t(1) << 24);
-      limit = bias_room_start(S, chunks, k);
-      if (limit > INT32_MAX) limit = INT32_MAX;  // 32-bit list offsets (rows past it: recomputed)
-      streaming = sizeof(int64_t) * (size_t)S + 2 * sizeof(int32_t) * (size_t)S +
-                  (sizeof(float) + sizeof(int32_t)) * (size_t)limit;
-    }
-    ws.cand.ensure(chunked > streaming ? chunked : streaming);
-    if (stream) {
-      cand.base = ws.cand.as<int64_t>();
-      cand.cnt = reinterpret_cast<int32_t *>(cand.base + S);
-      cand.cap = cand.cnt + S;
-      cand.key = reinterpret_cast<float *>(cand.cap + S);
-      cand.idx = reinterpret_cast<int32_t *>(cand.key + limit);
-      cand.limit = limit;
-      // test hook, read per hop: DGS_BIAS_TEST_CAP=n limits a streamed row's list to n entries
-      // (n < k forces the exact recomputation of every streamed row)
-      const char *e = getenv("DGS_BIAS_TEST_CAP");
-      cand.cap_max = e ? atoll(e) : INT64_MAX;
-    }
+    const int64_t chunks =
+        src.num_edges > 0 ? src.num_edges / kStreamChunk + S : (int64_t(1) << 24);
+    int64_t limit = bias_room_start(S, chunks, k);
+    if (limit > INT32_MAX) limit = INT32_MAX;  // 32-bit list offsets (rows past it: recomputed)
+    ws.cand.ensure(sizeof(int64_t) * (size_t)S + 2 * sizeof(int32_t) * (size_t)S +
+                   (sizeof(float) + sizeof(int32_t)) * (size_t)limit);
+    cand.base = ws.cand.as<int64_t>();
+    cand.cnt = reinterpret_cast<int32_t *>(cand.base + S);
+    cand.cap = cand.cnt + S;
+    cand.key = reinterpret_cast<float *>(cand.cap + S);
+    cand.idx = reinterpret_cast<int32_t *>(cand.key + limit);
+    cand.limit = limit;
+    // test hook, read per hop: DGS_BIAS_TEST_CAP=n limits a row's list to n entries (n < k
+    // forces the exact recomputation of every hub row)
+    const char *e = getenv("DGS_BIAS_TEST_CAP");
+    cand.cap_max = e ? atoll(e) : INT64_MAX;
   }
   const PrepArgs pa{src, seeds, Sc, k, (int)replace,
                     use_hubs ? 1 : (bias_hubs ? 2 : 0),
@@ -1936,23 +1548,14 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     const dim3 grid((unsigned)ceil_div(S, kBiasRowsPerBlock));
     BiasHubArgs ba{};
     if (bias_hubs) {
-      const int64_t slots = nworkers + S;
-      float *ckey = ws.cand.as<float>();
-      int32_t *cidx = reinterpret_cast<int32_t *>(ckey + slots * k);
-      int32_t *ccnt = cidx + slots * k;
-      int32_t *wfirst = ccnt + slots;
-      ba = BiasHubArgs{src, Sc, k, launch_seed, rowinfo, tpre, boff, hub, ckey, cidx, ccnt,
-                       wfirst, wfirst + S, nworkers, rowpos, col, table, cand};
-      if (stream) {
-        hipLaunchKernelGGL(k_bias_boot, dim3((unsigned)std::min<int64_t>(S, 4096)),
-                           dim3(kTileRows), 0, st, ba);
-        DGS_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_bias_stream, dim3(bias_stream_blocks()), dim3(kTileRows), 0, st, ba,
-                           (const int64_t *)bsum, boff, d_nnz);
-      } else {
-        hipLaunchKernelGGL(k_bias_hub, dim3(bias_hub_blocks()), dim3(kTileRows), 0, st, ba,
-                           (const int64_t *)bsum, boff, d_nnz);
-      }
+      ba = BiasHubArgs{src,  Sc,     k,   launch_seed, rowinfo, tpre, boff,
+                       hub,  nworkers, rowpos, col, table,   cand};
+      hipLaunchKernelGGL(k_bias_boot, dim3((unsigned)std::min<int64_t>(S, 4096)), dim3(kTileRows),
+                         0, st, ba);
+      DGS_LAUNCH_CHECK();
+      // (its workgroup 0 also does the hop's tile-offset scan)
+      hipLaunchKernelGGL(k_bias_stream, dim3(bias_stream_blocks()), dim3(kTileRows), 0, st, ba,
+                         (const int64_t *)bsum, boff, d_nnz);
       DGS_LAUNCH_CHECK();
     }
     if (replace) {
@@ -1991,11 +1594,6 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
                          (const int64_t *)nullptr);
     }
     DGS_LAUNCH_CHECK();
-    if (bias_hubs) {
-      hipLaunchKernelGGL(k_bias_hub_merge, dim3((unsigned)std::min<int64_t>(S, 2048)),
-                         dim3(kTileRows), 0, st, ba);
-      DGS_LAUNCH_CHECK();
-    }
   }
 }
 

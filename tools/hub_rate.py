@@ -115,7 +115,7 @@ if __name__ == "__main__":
     p.add_argument("--synthetic-hub", type=int, default=0)
     p.add_argument("--bias", action="store_true")
     p.add_argument("--kernel", default="k_hub_reservoir",
-                   help="kernel whose launches --report prices (k_bias_hub for --bias)")
+                   help="kernel whose launches --report prices (k_bias_stream for --bias)")
     p.add_argument("--rows", type=int, default=1)
     a = p.parse_args()
     report(a) if a.report else (synthetic(a) if a.synthetic_hub else run(a))

@@ -27,3 +27,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -- \
   python3 bench.py --no-cpu-baseline > $O/stats.log 2>&1 || { tail -20 $O/stats.log; exit 1; }
 step done
+step rocprof-bias
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_bias -- \
+  python3 bench.py --no-cpu-baseline --bias > $O/stats_bias.log 2>&1 || { tail -20 $O/stats_bias.log; exit 1; }
+step done-bias
