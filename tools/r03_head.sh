@@ -31,3 +31,10 @@ step rocprof-bias
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_bias -- \
   python3 bench.py --no-cpu-baseline --bias > $O/stats_bias.log 2>&1 || { tail -20 $O/stats_bias.log; exit 1; }
 step done-bias
+if [ -n "${AB_LIBS:-}" ]; then
+  step ab-uniform
+  timeout -k 10 900 python tools/ab_bench.py --rounds 3 -- $AB_LIBS > $O/ab_uniform.txt 2>&1 \
+    || { tail -20 $O/ab_uniform.txt; exit 1; }
+  grep MEDIAN $O/ab_uniform.txt
+fi
+step end
