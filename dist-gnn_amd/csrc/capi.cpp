@@ -358,6 +358,17 @@ int dgs_extract_edge_data(const int64_t *nids, int64_t n, const int64_t *indptr,
   });
 }
 
+int dgs_test_bias_bounds(const uint32_t *x, const float *p, const float *thr, int64_t n,
+                         float *key, float *key_lower, uint8_t *flags, void *stream) {
+  return guard([&] {
+    DGS_CHECK(n >= 0, "negative size");
+    if (n == 0) return;
+    test_bias_bounds(dev_ptr(x, "x"), dev_ptr(p, "p"), dev_ptr(thr, "thr"), n,
+                     dev_ptr(key, "key"), dev_ptr(key_lower, "key_lower"), dev_ptr(flags, "flags"),
+                     S(stream));
+  });
+}
+
 int dgs_compute_frontier_heat(const int64_t *seeds, int64_t n_seeds, const int64_t *indptr,
                               const int64_t *indices, const float *probs,
                               const float *seeds_heat, int64_t num_nodes, int64_t num_picks,

@@ -111,6 +111,10 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count S, int64_t k, boo
                 const Table &table, HopScratch &ws, hipStream_t st,
                 const RelabelTail *tail = nullptr);
 
+// Test-only: exact A-Res keys, their lower bounds and the biased kernels' reject tests.
+void test_bias_bounds(const uint32_t *x, const float *p, const float *thr, int64_t n, float *key,
+                      float *key_low, uint8_t *flags, hipStream_t st);
+
 // Clean relabel table with capacity for n_ub insertions (marks the scratch dirty until the
 // hop's relabel pass has returned the touched slots to empty).
 Table relabel_table(HopScratch &ws, int64_t n_ub, hipStream_t st);

@@ -605,11 +605,13 @@ __device__ __forceinline__ bool ares_better(float ka, int32_t ia, float kb, int3
 // slack factor folded into the threshold once: thr_s = slack_thr(thr) = thr * (1 + 2^-16) (one
 // more rounding, 2^-24 relative, far inside the 2^-16 slack).  p <= 0 fails the p > 0 test;
 // thr = -inf gives a NaN or -inf bound, which the callers never test (they filter only once
-// the threshold is finite).
+// the threshold is finite).  A NaN bound lets the edge through: p = +inf with thr = 0 makes
+// p * thr NaN while the edge's key (+-0) ties thr (round 3: `>=` dropped it;
+// tests/test_gpu_parity.py::test_bias_filter_bounds_are_sound).
 __device__ __forceinline__ float slack_thr(float thr) { return thr * 1.0000152587890625f; }
 __device__ __forceinline__ bool ares_may_pass_s(float u, float p, float thr_s) {
   return (p > 0.0f) &
-         (__builtin_amdgcn_logf(u) >= __builtin_fmaf(p, thr_s, -0.0000152587890625f));
+         !(__builtin_amdgcn_logf(u) < __builtin_fmaf(p, thr_s, -0.0000152587890625f));
 }
 
 // (a & mask) | (b & ~mask): one v_bfi_b32
@@ -1129,6 +1131,18 @@ __device__ __forceinline__ void tree_merge8(const HalfTopK &top, int64_t k, int 
   }
 }
 
+// The stream kernel's reject test, in the draw's own domain.  ln u <= u - 1 gives log2 u < p T
+// whenever u < 1 + p T ln2, and u = RN(x 2^-32 + 2^-33) < 1 + p T ln2 (1 + 2^-16) - 2^-20
+// follows from (float)x < p cx + bx with cx = lin_cx(T) and bx = 2^32 (1 - 2^-20) - 512: the
+// margins cover u's rounding, the fma's and the fixed-operation log2's error.  So a rejected
+// edge has key < T.  p <= 0 or NaN only lets an edge through (its key is exact later).
+__device__ __forceinline__ float lin_cx(float T) {
+  return T * (0.6931471805599453f * 1.0000152587890625f) * 4294967296.0f;
+}
+__device__ __forceinline__ bool lin_reject(uint32_t x, float p, float cx) {
+  return (float)x < __builtin_fmaf(p, cx, 4294962688.0f);
+}
+
 // A value <= ares_key(u, p) for every u in (0, 1] and p: the hardware log2 (v_log_f32, within a
 // few ulp of dgs_log2f) lowered by 2^-16 relative + 2^-16 absolute, divided through the hardware
 // reciprocal and lowered by another 2^-16 relative -- margins far above every rounding on the way
@@ -1275,7 +1289,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
     kk = c.kk;
     pr = c.pr;
     T = key_from_order((int32_t)a.hub.thr[hh]);
-    cx = T * (0.6931471805599453f * 1.0000152587890625f) * 4294967296.0f;
+    cx = lin_cx(T);
     // no finite sample threshold (weights <= 0): every edge would be a candidate; the merge
     // recomputes the row instead (every worker of the row stores the same marker)
     skip = !(T > -__builtin_inff());
@@ -1333,17 +1347,12 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
 #pragma unroll
     for (int e = 0; e < kStreamT + 1; ++e) w2[e] = bitsel(m2, wv[e + 2], wv[e]);
     uint32_t m = 0;  // bit t: edge i0 + 32 t passed the cheap bound
-    // Reject when key < T is certain, in the draw's own domain: ln u <= u - 1 gives
-    // log2 u < p T  whenever  u < 1 + p T ln2, and u = RN(x 2^-32 + 2^-33) < 1 + p T ln2 (1 +
-    // 2^-16) - 2^-20 follows from (float)x < p cx + bx (bx = 2^32 (1 - 2^-20) - 512: the margins
-    // cover u's rounding, the fma's and the fixed-operation log2's error).  One convert, one fma
-    // and one compare per edge; p <= 0 or NaN only lets an edge through (its key is exact later).
-    // (Round 3 A/B against the hardware-log2 bound: stream kernel 35.1 -> 33.5 us, +1.7 %.)
+    // Reject when key < T is certain (lin_reject: one convert, one fma and one compare per
+    // edge; round 3 A/B against the hardware-log2 bound: stream kernel 35.1 -> 33.5 us, +1.7 %).
 #pragma unroll
     for (int t = 0; t < kStreamT; ++t) {
-      const float xf = (float)bitsel(m1, w2[t + 1], w2[t]);
       const bool valid = whole | (i0 + 32u * t < deg);
-      m |= (uint32_t)(valid & !(xf < __builtin_fmaf(p[t], cx, 4294962688.0f))) << t;
+      m |= (uint32_t)(valid & !lin_reject(bitsel(m1, w2[t + 1], w2[t]), p[t], cx)) << t;
     }
 
     // the few that pass the bound go to the row's list as (u, edge); the merge computes their
@@ -1455,7 +1464,30 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
   stream_merge_block(a, blockIdx.x, gridDim.x);
 }
 
+// Test-only (dgs_test_bias_bounds): the exact A-Res key, key_lower() and the two reject tests
+// the biased kernels use (bit 0: the stream kernel's lin_reject against T; bit 1: the row /
+// hub-run filter !ares_may_pass_s against thr = T), per (draw x, probability p, threshold T).
+__global__ void k_test_bias_bounds(const uint32_t *x, const float *p, const float *thr, int64_t n,
+                                   float *key, float *klow, uint8_t *flags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float u = curand_uniform_from(x[i]);
+  const float pi = p[i], T = thr[i];
+  key[i] = ares_key(u, pi);
+  klow[i] = key_lower(u, pi);
+  flags[i] = (uint8_t)((int)lin_reject(x[i], pi, lin_cx(T)) |
+                       ((int)!ares_may_pass_s(u, pi, slack_thr(T)) << 1));
+}
+
 }  // namespace
+
+void test_bias_bounds(const uint32_t *x, const float *p, const float *thr, int64_t n, float *key,
+                      float *key_low, uint8_t *flags, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_test_bias_bounds, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, x, p,
+                     thr, n, key, key_low, flags);
+  DGS_LAUNCH_CHECK();
+}
 
 // ------------------------------------------------------------------------------------
 void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bool replace,

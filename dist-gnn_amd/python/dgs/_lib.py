@@ -53,6 +53,7 @@ _SIGS = {
     "dgs_relabel": (c_int, [p_vp, p_i64, c_int, p_vp, p_i64, c_int, c_vp, p_i64, p_vp, c_vp]),
     "dgs_extract_indptr": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp]),
     "dgs_extract_edge_data": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "dgs_test_bias_bounds": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "dgs_compute_frontier_heat": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                           c_i64, c_vp, c_vp]),
     "dgs_compute_frontier_heat_fixed": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,

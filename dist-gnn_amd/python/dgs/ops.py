@@ -18,7 +18,7 @@ __all__ = [
     "_CAPI_cuda_sample_neighbors_bias", "_CAPI_cuda_sampled_tensor_relabel",
     "_CAPI_cuda_index_select", "_Test_Randn", "_Test_NCCLTensorAllGather",
     "_Test_GetLocalRank", "_Test_GetWorldSize", "_Test_ExtractEdgeData", "_Test_ExtractIndptr",
-    "_CAPI_set_random_seed", "_CAPI_set_host_comm", "draw_launch_seeds",
+    "_CAPI_set_random_seed", "_CAPI_set_host_comm", "draw_launch_seeds", "_Test_BiasKeyBounds",
 ]
 
 # host storage registered by _CAPI_tensor_pin_memory: data_ptr -> (the tensor, the registered
@@ -285,6 +285,28 @@ def _Test_ExtractEdgeData(nids, indptr, sub_indptr, edge_data):
     check(lib.dgs_extract_edge_data(ptr(n), n.numel(), ptr(ip), ptr(sp), ptr(ed),
                                     ed.element_size(), ptr(out), stream_ptr(dev)))
     return out
+
+
+def _Test_BiasKeyBounds(x, p, thr):
+    """ADDITIVE test op (include/dgs_amd.h dgs_test_bias_bounds): for 32-bit draws x (int64
+    values in [0, 2^32)), probabilities p and thresholds thr (float32, CUDA, equal sizes) ->
+    (exact A-Res key, its lower bound, reject flags: bit 0 streamed-hub filter, bit 1 row
+    filter, each set only when the key is certainly below thr)."""
+    for t, name in ((x, "x"), (p, "p"), (thr, "thr")):
+        check_cuda(t, name)
+    if not (x.numel() == p.numel() == thr.numel()):
+        raise RuntimeError("x, p and thr need equal sizes")
+    if p.dtype != torch.float32 or thr.dtype != torch.float32:
+        raise RuntimeError("p and thr must be float32")
+    xi = x.to(torch.int64)
+    x32 = torch.where(xi >= 2 ** 31, xi - 2 ** 32, xi).to(torch.int32).contiguous()
+    pc, tc = p.contiguous(), thr.contiguous()
+    key = torch.empty_like(pc)
+    low = torch.empty_like(pc)
+    flags = torch.empty(pc.numel(), dtype=torch.uint8, device=pc.device)
+    check(lib.dgs_test_bias_bounds(ptr(x32), ptr(pc), ptr(tc), pc.numel(), ptr(key), ptr(low),
+                                   ptr(flags), stream_ptr(pc.device)))
+    return key, low, flags
 
 
 # ------------------------------------------------------------------ heat

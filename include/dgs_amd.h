@@ -117,6 +117,15 @@ int dgs_extract_edge_data(const int64_t *nids, int64_t n, const int64_t *indptr,
                           const int64_t *sub_indptr, const void *edge_data, int64_t elem_bytes,
                           void *sub_edge_data, void *stream);
 
+/* Test-only (no reference counterpart; a _Test_ op like _Test_ExtractIndptr): for each i < n,
+ * key[i] = the A-Res key of draw x[i] under probability p[i] (the definition the biased
+ * samplers and the oracle share), key_lower[i] = the provable lower bound the biased hub
+ * sampling threshold is built from, and flags[i] bit 0 / bit 1 = the streamed hub filter's /
+ * the row filter's "certainly below thr[i]" verdict.  Device arrays; the bits must only be set
+ * when key[i] < thr[i] (tests/test_gpu_parity.py::test_bias_filter_bounds_are_sound). */
+int dgs_test_bias_bounds(const uint32_t *x, const float *p, const float *thr, int64_t n,
+                         float *key, float *key_lower, uint8_t *flags, void *stream);
+
 /* replaces cache::cuda::ComputeFrontierHeat[WithBias] (preprocess_heat.cu:35-56,100-121;
  * _CAPI_compute_frontier_heat[_with_bias]).  probs == NULL selects the unbiased form.
  * frontier_heat[num_nodes] is overwritten. */

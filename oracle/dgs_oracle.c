@@ -189,6 +189,11 @@ float oracle_ares_key(float u, float p) {
   return oracle_log2f(u) / p;
 }
 
+/* vectorised oracle_ares_key (test helper) */
+void oracle_ares_keys(const float *u, const float *p, float *out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = oracle_ares_key(u[i], p[i]);
+}
+
 static inline int ares_better(float ka, int64_t ia, float kb, int64_t ib) {
   return ka > kb || (ka == kb && ia < ib);
 }

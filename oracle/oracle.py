@@ -115,6 +115,24 @@ def ares_key(u, p):
     return lib().oracle_ares_key(u, p)
 
 
+def curand_uniform_of(x):
+    """curand_uniform() of raw 32-bit draws x (uint32 array): RN(float(x) 2^-32 + 2^-33) -- the
+    scaled float is exact, so one float64 sum rounded once to float32 reproduces the fma."""
+    xf = np.asarray(x, dtype=np.uint64).astype(np.float32).astype(np.float64)
+    return (xf * 2.0 ** -32 + 2.0 ** -33).astype(np.float32)
+
+
+def ares_keys(u, p):
+    """Vectorised ares_key (float32 arrays)."""
+    u = np.ascontiguousarray(u, dtype=np.float32)
+    p = np.ascontiguousarray(p, dtype=np.float32)
+    out = np.empty_like(u)
+    f = ctypes.POINTER(ctypes.c_float)
+    lib().oracle_ares_keys(u.ctypes.data_as(f), p.ctypes.data_as(f), out.ctypes.data_as(f),
+                           ctypes.c_int64(u.size))
+    return out
+
+
 # ---------------------------------------------------------------- sampling
 def sample_uniform(seeds, indptr, indices, k, replace, launch_seed, nthreads=1):
     seeds, indptr, indices = _i64(seeds), _i64(indptr), _i64(indices)

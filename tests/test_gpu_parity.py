@@ -116,9 +116,9 @@ def test_sample_neighbors_bias(dgs, k, replace):
 
 def _bias_hub_graph(seed):
     """Biased hub rows of every class of the streaming scheme (csrc/sample.hip): rows the boot
-    kernel solves outright (2048 < deg <= 8192), streamed rows (deg > 8192) up to 250K edges,
-    a streamed row with all-zero weights (no finite sample threshold) and one with only three
-    positive weights, plus ordinary rows."""
+    kernel's sample covers whole (deg <= 4096) and larger ones up to 250K edges, a row with
+    all-zero weights (no finite sample threshold) and one with only three positive weights,
+    rows with infinite weights (tied keys), plus ordinary rows."""
     rng = np.random.default_rng(seed)
     degs = rng.integers(0, 60, 300)
     hubs = [2049, 3000, 5000, 8192, 8193, 9000, 20000, 30000, 70000, 250000]
@@ -132,6 +132,12 @@ def _bias_hub_graph(seed):
     probs[indptr[7] + np.array([5, 17000, 29999])] = [0.5, 2.0, 1.0]
     # deg 70000: weights rising along the row (a prefix sample would be unrepresentative)
     probs[indptr[8]:indptr[9]] = np.linspace(0.01, 50.0, 70000, dtype=np.float32)
+    # infinite weights (keys +-0, tied: picked by edge index): 40 in a streamed row, 20 in a row
+    # the boot covers whole, 3 in a small row
+    probs[indptr[5] + rng.choice(9000, 40, replace=False)] = np.inf
+    probs[indptr[2] + rng.choice(5000, 20, replace=False)] = np.inf
+    small = int(np.argmax(degs[10:] >= 40)) + 10
+    probs[indptr[small] + np.array([0, 7, 30])] = np.inf
     return indptr, indices, probs
 
 
@@ -155,6 +161,51 @@ def test_bias_hub_rows_streaming(dgs, k, cap, monkeypatch):
         er, ec = O.sample_bias(seeds, indptr, indices, probs, k, False, ls)
         assert np.array_equal(row.cpu().numpy(), er)
         assert np.array_equal(col.cpu().numpy(), ec)
+
+
+def test_bias_filter_bounds_are_sound(dgs):
+    """The biased kernels' only inequalities: the hub sampling threshold is built from
+    key_lower() (it must never exceed the exact key), and edges are dropped by two cheap tests
+    (they must only fire when the exact key is strictly below the threshold, ties included).
+    4 M random draws with log-uniform and integer (degree-like) weights plus edge values of both
+    (0, -1, denormals, the key_lower range limits, 1e38, inf, NaN; draws at 0 and near 2^32),
+    each against thresholds at and around its own exact key, which must also match the oracle
+    bit for bit."""
+    rng = np.random.default_rng(31)
+    n = 1 << 22
+    x = rng.integers(0, 2 ** 32, n, dtype=np.uint64)
+    ex = np.array([0, 1, 2, 255, 256, 2 ** 31 - 1, 2 ** 31, 2 ** 32 - 1, 2 ** 32 - 2, 2 ** 32 - 128,
+                   2 ** 32 - 129, 2 ** 32 - 256, 2 ** 32 - 512, 2 ** 32 - 4608, 2 ** 32 - 4609,
+                   2 ** 32 - 8192], dtype=np.uint64)
+    p = np.exp(rng.uniform(np.log(1e-6), np.log(1e6), n)).astype(np.float32)
+    p[1::3] = rng.integers(1, 200000, p[1::3].size).astype(np.float32)
+    ep = np.array([0.0, -0.0, -1.0, 1e-45, 1e-40, 7.8e-31, 7.888609052210118e-31, 1e-30, 0.5, 1.0,
+                   1e30, 1.2676506002282294e30, 1.3e30, 1e38, np.inf, np.nan], dtype=np.float32)
+    # every edge draw with every edge weight, repeated at the front
+    gx, gp = np.meshgrid(ex, ep)
+    m = gx.size
+    x[:m], p[:m] = gx.ravel(), gp.ravel()
+    x[m:2 * m], p[m:2 * m] = gx.ravel(), rng.uniform(0.5, 3.0, m).astype(np.float32)
+    key = O.ares_keys(O.curand_uniform_of(x), p)
+    # thresholds at, just above / below and around each key; -inf keys get random thresholds
+    fac = np.array([1.0, 1.0 + 2 ** -24, 1.0 - 2 ** -24, 1.0 + 2 ** -20, 1.0 - 2 ** -20,
+                    1.0 + 2 ** -16, 1.0 - 2 ** -16, 1.0 + 2 ** -12, 1.0 - 2 ** -12, 1.5, 0.5, 4.0],
+                   dtype=np.float32)
+    thr = key * fac[rng.integers(0, fac.size, n)]
+    ties = rng.random(n) < 0.2
+    thr[ties] = key[ties]
+    bad = ~np.isfinite(thr)
+    thr[bad] = -np.exp(rng.uniform(np.log(1e-9), np.log(1e3), int(bad.sum()))).astype(np.float32)
+    thr[:16] = 0.0
+    gk, gl, gf = dgs.ops._Test_BiasKeyBounds(_cuda(x.astype(np.int64)), _cuda(p), _cuda(thr))
+    gk, gl, gf = gk.cpu().numpy(), gl.cpu().numpy(), gf.cpu().numpy()
+    assert np.array_equal(gk.view(np.uint32), key.view(np.uint32)), "exact key differs from oracle"
+    assert not np.isnan(gk).any()
+    assert (gl <= gk).all(), "key_lower above the exact key"
+    for bit, name in ((1, "streamed-hub filter"), (2, "row filter")):
+        fired = (gf & bit) != 0
+        assert (gk[fired] < thr[fired]).all(), f"{name} dropped an edge whose key reaches thr"
+        assert fired.mean() > 0.05, f"{name} never fires (test inputs too weak)"
 
 
 def test_sample_golden_vectors(dgs):
