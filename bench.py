@@ -241,6 +241,32 @@ def hot_set(indices, N, frac, dev):
     return torch.sort(indeg, descending=True, stable=True).indices[:n_hot].cpu()
 
 
+def verify_setup(sampler, server, indices, feats, s_cache, f_cache, N, dev):
+    """The HBM copies the services made from the host inputs (read by the GPU through the
+    registered host pages) equal the inputs as torch copies them: the sampler's cached
+    neighbour ids (when it caches every row in id order) and the feature server's cached rows.
+    A mismatch ends the run before anything is timed."""
+    _, sub_indices, _ = sampler._CAPI_get_local_cache_structure_tensors()
+    if s_cache.numel() == N and torch.equal(s_cache, torch.arange(N)):
+        want = indices.to(dev)
+        bad = int((sub_indices != want).sum()) if sub_indices.numel() == want.numel() else -1
+        if bad:
+            raise SystemExit(f"bench.py: the sampler's HBM copy of the graph differs from the "
+                             f"host graph at {bad} of {want.numel()} neighbour ids")
+        del want
+    gpu_feat = server._CAPI_get_gpu_feature()
+    if gpu_feat is not None and f_cache.numel():
+        rows = 0
+        for part in torch.split(f_cache, 1 << 20):  # bounded temporaries
+            want = feats[part].to(dev)
+            got = gpu_feat[rows: rows + part.numel()]
+            if not torch.equal(got, want):
+                raise SystemExit("bench.py: the feature server's HBM cache differs from the host "
+                                 f"features in rows {rows}..{rows + part.numel()}")
+            rows += part.numel()
+    torch.cuda.synchronize()
+
+
 # ---------------------------------------------------------------------------- timed run
 def timed_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist, profile):
     """W warm-up batches, then exactly K timed batches between barrier + synchronize on both
@@ -397,6 +423,7 @@ def main():
     layout = server._layout()
     torch.cuda.synchronize()
     log(f"[bench] services ready in {time.time() - t0:.1f}s (mode {mode})")
+    verify_setup(sampler, server, indices, feats, s_cache, f_cache, N, dev)
     dgs.ops._CAPI_set_random_seed(args.seed + rank)
 
     torch.manual_seed(1)
@@ -765,4 +792,16 @@ def cpu_baseline(indptr, indices, probs, feats, train, fan_out, args):
 
 
 if __name__ == "__main__":
-    main()
+    if os.environ.get("WORLD_SIZE", "1") != "1":
+        # a failed rank exits at once: unwinding would wait in teardown collectives for ranks
+        # that are themselves waiting for it
+        try:
+            main()
+        except BaseException:
+            import traceback
+            traceback.print_exc()
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(1)
+    else:
+        main()

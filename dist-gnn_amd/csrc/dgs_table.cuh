@@ -43,6 +43,12 @@ struct RelabelTail {
   const int64_t *unique;    // the hop's unique ids (first-occurrence order)
   const int64_t *d_nuniq;   // their count (device)
   int64_t nblk;  // 256-thread blocks covering S + nnz (upper bounds; >= nnz and >= U)
+  // an id outside [0, t.n) (never produced by a correct hop) stores bad_tag to *bad, if set
+  int64_t *bad = nullptr;
+  int64_t bad_tag = 0;
+  // diagnostics of the first such id: {taken, hop, edge, id, nnz, row}
+  int64_t *dbg = nullptr;
+  int64_t hop = 0;
 };
 
 #ifdef __HIPCC__
@@ -50,17 +56,39 @@ struct RelabelTail {
 __device__ __forceinline__ int32_t *dval(const Table &t, int64_t x) { return t.val + 2 * x; }
 __device__ __forceinline__ int32_t *dlab(const Table &t, int64_t x) { return t.val + 2 * x + 1; }
 
+// Ids are range-checked before they index the table (one compare each): a corrupt id yields -1
+// in the output instead of an address outside the table.
 __device__ __forceinline__ void relabel_tail_block(const RelabelTail &r, int64_t blk) {
   const int64_t nb = *r.d_nb;
   const int64_t nu = *r.d_nuniq;
   const int64_t e = blk * 256 + threadIdx.x;
+  const uint64_t n = (uint64_t)r.t.n;
   if (e < nb) {
     const int64_t v = r.out_col[e];
-    r.out_col[e] = *dlab(r.t, v);
-    if (r.remap_rows) r.out_row[e] = *dlab(r.t, r.seeds[r.out_row[e]]);
+    bool ok = (uint64_t)v < n;
+    r.out_col[e] = ok ? *dlab(r.t, v) : -1;
+    if (r.remap_rows) {
+      const int64_t row = r.out_row[e];
+      const int64_t x = (uint64_t)row < (uint64_t)r.Sc.get() ? r.seeds[row] : -1;
+      ok &= (uint64_t)x < n;
+      r.out_row[e] = (uint64_t)x < n ? *dlab(r.t, x) : -1;
+    }
+    if (!ok && r.bad) {
+      *r.bad = r.bad_tag;
+      if (r.dbg && atomicCAS(reinterpret_cast<unsigned long long *>(r.dbg), 0ull, 1ull) == 0ull) {
+        r.dbg[1] = r.hop;
+        r.dbg[2] = e;
+        r.dbg[3] = v;
+        r.dbg[4] = nb;
+        r.dbg[5] = r.remap_rows ? r.out_row[e] : -1;
+      }
+    }
   }
   // (the label loads above read the other word of the pair: no conflict with the resets)
-  if (e < nu) *dval(r.t, r.unique[e]) = kTableNoPos;
+  if (e < nu) {
+    const int64_t u = r.unique[e];
+    if ((uint64_t)u < n) *dval(r.t, u) = kTableNoPos;
+  }
 }
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
@@ -96,7 +124,9 @@ __device__ __forceinline__ void table_record(const Table &t, int64_t x, int64_t 
   if (t.direct) {
     // val only decreases: skip the atomic when an earlier occurrence is already recorded.  (A
     // no-return atomic without the check measured 1.8x slower on the last hop: hot nodes
-    // recur ~1000 times per hop and same-address atomics serialise.)
+    // recur ~1000 times per hop and same-address atomics serialise.)  Ids outside [0, n) are
+    // not recorded (a corrupt id must not address memory outside the table).
+    if ((uint64_t)x >= (uint64_t)t.n) return;
     int32_t *v = dval(t, x);
     if (*v > (int32_t)pos) atomicMin(v, (int32_t)pos);
   } else if (t.key) {

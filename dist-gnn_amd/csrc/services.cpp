@@ -232,6 +232,9 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
   sample_end(L, sizes, st);
 }
 
+// device words after the sizes and the bad-seed word: the relabel pass's diagnostics
+constexpr int kSizesDbg = 8;
+
 // Enqueues every hop of one call on `st` and returns: the call's sizes are read by
 // sample_end.  One call per stream may be outstanding (its context holds the published sizes).
 void Sampler::sample_begin(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_out,
@@ -349,8 +352,9 @@ void Sampler::launch(Ctx &c, const Job &j, hipStream_t st) {
   int64_t *const *cols = j.cols.data();
   const uint64_t *hop_seed = j.hop_seed.data();
   // device sizes: 3 per hop, then the bad-seed word (holds the seq of the last call that saw
-  // a seed outside [0, num_nodes); zeroed at allocation, never reset)
-  if (c.sizes.ensure(sizeof(int64_t) * (size_t)(3 * L + 1)))
+  // a seed outside [0, num_nodes), or -seq of the last call whose relabel met a sampled id
+  // outside it (an internal error); zeroed at allocation, never reset)
+  if (c.sizes.ensure(sizeof(int64_t) * (size_t)(3 * L + 1 + kSizesDbg)))
     DGS_HIP(hipMemsetAsync(c.sizes.p, 0, c.sizes.bytes, st));
   if (c.sizes_host.bytes < sizeof(int64_t) * (size_t)(3 * L + 2)) {
     c.sizes_host.flags = hipHostMallocCoherent | hipHostMallocMapped;
@@ -392,7 +396,14 @@ void Sampler::launch(Ctx &c, const Job &j, hipStream_t st) {
     const bool last = h == L - 1;
     const HostSizes pub = last ? HostSizes{dsz, 3 * L + 1, c.sizes_host_dev, seq} : HostSizes{};
     relabel_hop(cur, S, cols[h], d_nnz, nnz_cap, /*seeds_unique=*/h > 0, t, frontiers[h],
-                rows[h], cols[h], d_uniq, c.ws, st, pub, last ? nullptr : &tail);
+                rows[h], cols[h], d_uniq, c.ws, st, pub, &tail);
+    tail.bad = src.bad;
+    tail.bad_tag = -(int64_t)seq;
+    tail.dbg = dsz + 3 * L + 1;
+    tail.hop = h;
+    // the last hop's pass runs after the sizes were published: its flag is seen by the
+    // stream's next call
+    if (last) launch_relabel_tail(tail, st);
     have_tail = !last;
     if (last) c.dirty[tb] = false;
     cur = frontiers[h];
@@ -447,6 +458,14 @@ void Sampler::sample_end(int L, int64_t *sizes, hipStream_t st) {
   // reference reads out of bounds instead).
   DGS_CHECK(hsz[1 + 3 * L] != (int64_t)seq,
             "sample: a seed is outside [0, num_nodes)");
+  if (hsz[1 + 3 * L] < 0) {
+    int64_t d[kSizesDbg] = {};
+    (void)hipMemcpy(d, c.sizes.as<int64_t>() + 3 * L + 1, sizeof(d), hipMemcpyDeviceToHost);
+    DGS_CHECK(false, "sample: internal error: a sampled neighbour id was outside [0, num_nodes) "
+                         "(first: hop " + std::to_string(d[1]) + " edge " + std::to_string(d[2]) +
+                         " id " + std::to_string(d[3]) + " nnz " + std::to_string(d[4]) +
+                         " row " + std::to_string(d[5]) + ")");
+  }
   int64_t s = n_seeds;
   for (int h = 0; h < L; ++h) {
     sizes[3 * h + 0] = s;
