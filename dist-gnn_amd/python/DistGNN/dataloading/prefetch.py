@@ -92,10 +92,15 @@ class PrefetchLoader:
             return _raw_stream(self._dev)
         return torch.cuda.current_stream(self.device).cuda_stream
 
-    # Stream ordering (no record_stream on the outputs): every output is allocated on the
-    # caller's stream C and then written on the batch stream B only after B waits for C
-    # (dgs.ops._stream_wait, recorded after the allocations, so C's earlier users of the
-    # memory are done); C waits for B before the outputs are handed out or dropped.
+    # Stream ordering.  A batch's sample outputs are allocated from the pool of the batch stream
+    # B that writes them, and recorded on the caller's stream C when handed out: the caching
+    # allocator then reuses that memory only after both streams' uses (its own event queries).
+    # (Allocated on C instead, a block the previous batch's feature gather still writes -- x is
+    # dropped by the caller as soon as the gather is enqueued -- could be handed to the next
+    # batch, whose sampler would then race that gather unless B's wait for C held exactly;
+    # observed as feature bits in a batch's neighbour ids with two processes on one GPU.)
+    # B still waits for C before the launches (the seeds may be produced on C), and C waits
+    # for B before the outputs are used.
     def _submit(self):
         try:
             seeds = next(self._seeds)
@@ -108,8 +113,11 @@ class PrefetchLoader:
         cur = self._caller_stream()
         # the caller may drop its seeds at once: their memory must outlive B's reads
         seeds.record_stream(self._streams[w])
-        # int64 seeds + one output buffer, on C
-        prep = self.sampler._prepare(seeds, self.fan_out, packed=True)
+        # int64 seeds (converted on C if need be) + one output buffer from B's pool
+        prep = self.sampler._prepare(seeds, self.fan_out, packed=True,
+                                     alloc_stream=self._streams[w])
+        if prep[0] is not seeds:
+            prep[0].record_stream(self._streams[w])
         # B waits for C (after the allocations), then the call is enqueued: one C-ABI call.
         # B is not touched again before result(): the sampler's launcher thread may issue
         # the launches.  The sampler draws the launch seeds once it has accepted the call.
@@ -129,12 +137,15 @@ class PrefetchLoader:
         pending, s64, w = self._inflight.popleft()
         st = self._st[w]
         cur = self._caller_stream()
+        buf = pending._buf
         try:
             blocks = pending.result(cast=False)
         except BaseException:
             dgs.ops._stream_wait(st, cur)
             self.close()
             raise
+        if buf is not None:  # the outputs' memory is used on C from here on
+            buf.record_stream(torch.cuda.current_stream(self.device))
         # C after B (the sample call); the feature and label gathers then run on C, whose
         # hardware queue the batch streams do not use -- the wait and both gathers in one
         # C-ABI call.  (The label gather depends on the seeds only; on C it stays off the

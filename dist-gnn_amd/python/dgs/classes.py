@@ -157,8 +157,10 @@ class P2PCacheSampler:
                                      int(bool(replace)), *ptrs, sizes, stream_ptr(s.device)))
         return self._views(seeds, buf, caps, total, sizes, L)
 
-    def _prepare(self, seeds, fan_out, packed=False):
-        """packed: no per-hop pointer arrays (the buffer goes to the C ABI whole)."""
+    def _prepare(self, seeds, fan_out, packed=False, alloc_stream=None):
+        """packed: no per-hop pointer arrays (the buffer goes to the C ABI whole).
+        alloc_stream: a torch stream whose pool the output buffer comes from (the stream the
+        call writes it on; default the current stream)."""
         check_cuda(seeds, "seeds")
         s = seeds if seeds.dtype == torch.int64 and seeds.is_contiguous() else \
             as_i64(seeds, "seeds")
@@ -176,7 +178,11 @@ class P2PCacheSampler:
             self._plans[key] = plan
         fo, caps, total = plan
         # one allocation for every hop's (frontier, row, col) buffers
-        buf = torch.empty(max(total, 1), dtype=torch.int64, device=s.device)
+        if alloc_stream is None:
+            buf = torch.empty(max(total, 1), dtype=torch.int64, device=s.device)
+        else:
+            with torch.cuda.stream(alloc_stream):
+                buf = torch.empty(max(total, 1), dtype=torch.int64, device=s.device)
         return s, L, fo, caps, total, buf, None if packed else plan_ptrs(buf.data_ptr(), caps)
 
     def _views(self, seeds, buf, caps, total, sizes, L, cast=True):
