@@ -203,8 +203,7 @@ def test_begin_end_protocol(dgs, host_async):
 
 
 def test_prefetch_outputs_survive_caller_memory_reuse(dgs):
-    """Outputs are allocated on the caller's stream and written on batch streams ordered after
-    it: a caller that drops each batch at once and fills freshly allocated memory on its stream
+    """A caller that drops each batch at once and fills freshly allocated memory on its stream
     (a training step recycling the blocks) must not corrupt the batches still in flight, and a
     loader closed mid-way leaves the memory it dropped safe to reuse."""
     from DistGNN.dataloading import PrefetchLoader
@@ -324,3 +323,41 @@ def test_prefetch_submit_error_surfaces_once(dgs):
     it.close()
     with pytest.raises(StopIteration):
         next(it)
+
+
+def test_prefetch_wide_gather_dropped_at_once(dgs):
+    """The hazard behind the round-3 N = 2 fault: the caller drops x while its (long, wide)
+    gather is still running, and the next batches' sample outputs must not land in that memory
+    before the gather is done.  Feature rows of 16 KiB make every gather tens of MB; the
+    batches must equal the sequential loop's, with no id left unwritten (-1)."""
+    from DistGNN.dataloading import PrefetchLoader
+    indptr, indices, _ = _graph()
+    n = indptr.size - 1
+    sampler = dgs.classes.P2PCacheSampler(torch.from_numpy(indptr), torch.from_numpy(indices),
+                                          torch.Tensor(), torch.arange(n), 0)
+    dim = 4096
+    feats = torch.randn(n, dim, generator=torch.Generator().manual_seed(4))
+    server = dgs.classes.P2PCacheFeatureServer(feats, torch.arange(n), 0)
+    labels = torch.randint(0, 40, (n,), generator=torch.Generator().manual_seed(0)).cuda()
+    fan_out = [15, 10, 5]
+    batches = _batches(n, nb=24, bsz=128)
+    dgs.ops._CAPI_set_random_seed(13)
+    exp = []
+    for s in batches:
+        blocks = sampler._CAPI_sample_node_classifiction(s, fan_out, False)
+        exp.append(([tuple(t.cpu() for t in b) for b in blocks],
+                    float(server._CAPI_get_feature(blocks[-1][1]).double().sum())))
+    dgs.ops._CAPI_set_random_seed(13)
+    got = []
+    for blocks, x, _ in PrefetchLoader(sampler, batches, fan_out, server=server, labels=labels,
+                                       depth=3):
+        got.append(([tuple(t.cpu() for t in b) for b in blocks], float(x.double().sum())))
+        del blocks, x  # x's gather may still run: its memory goes back to the pool at once
+    torch.cuda.synchronize()
+    assert len(got) == len(exp)
+    for (gb, gx), (eb, ex) in zip(got, exp):
+        assert gx == ex
+        for tg, te in zip(gb, eb):
+            for u, v in zip(tg, te):
+                assert torch.equal(u, v)
+            assert int(tg[3].min()) >= 0 if tg[3].numel() else True
