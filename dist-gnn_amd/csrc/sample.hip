@@ -1599,10 +1599,51 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
       hipLaunchKernelGGL(k_bias_boot, dim3((unsigned)std::min<int64_t>(S, 4096)), dim3(kTileRows),
                          0, st, ba);
       DGS_LAUNCH_CHECK();
+      // DGS_BIAS_STATS=1 (diagnostics, synchronises): the hop's hub rows and their edges
+      static const bool stats = getenv("DGS_BIAS_STATS") != nullptr;
+      if (stats) {
+        DGS_HIP(hipStreamSynchronize(st));
+        int64_t packed = 0, Sd = S;
+        DGS_HIP(hipMemcpy(&packed, hub.count, 8, hipMemcpyDeviceToHost));
+        if (Sc.p) DGS_HIP(hipMemcpy(&Sd, Sc.p, 8, hipMemcpyDeviceToHost));
+        const int64_t H = (int64_t)((uint64_t)packed >> kHubShift);
+        std::vector<int64_t> rows((size_t)H);
+        std::vector<RowInfo> ri((size_t)Sd);
+        if (H) DGS_HIP(hipMemcpy(rows.data(), hub.row, 8 * H, hipMemcpyDeviceToHost));
+        if (Sd) DGS_HIP(hipMemcpy(ri.data(), rowinfo, sizeof(RowInfo) * Sd, hipMemcpyDeviceToHost));
+        int64_t edges = 0;
+        for (int64_t h = 0; h < H; ++h) {
+          const int64_t d = ri[(size_t)rows[(size_t)h]].dl & kOffMask;
+          edges += d;
+        }
+        fprintf(stderr, "[bias stats] S %lld hubs %lld hub edges %lld stream chunks %lld\n",
+                (long long)Sd, (long long)H, (long long)edges,
+                (long long)((uint64_t)packed & kHubChunkMask));
+      }
       // (its workgroup 0 also does the hop's tile-offset scan)
       hipLaunchKernelGGL(k_bias_stream, dim3(bias_stream_blocks()), dim3(kTileRows), 0, st, ba,
                          (const int64_t *)bsum, boff, d_nnz);
       DGS_LAUNCH_CHECK();
+      if (stats) {  // candidates per hub row after the stream
+        DGS_HIP(hipStreamSynchronize(st));
+        int64_t packed = 0;
+        DGS_HIP(hipMemcpy(&packed, hub.count, 8, hipMemcpyDeviceToHost));
+        const int64_t H = (int64_t)((uint64_t)packed >> kHubShift);
+        std::vector<int32_t> cnt((size_t)H), cap((size_t)H);
+        if (H) {
+          DGS_HIP(hipMemcpy(cnt.data(), cand.cnt, 4 * H, hipMemcpyDeviceToHost));
+          DGS_HIP(hipMemcpy(cap.data(), cand.cap, 4 * H, hipMemcpyDeviceToHost));
+        }
+        int64_t tot = 0, over = 0, mx = 0, big64 = 0;
+        for (int64_t h = 0; h < H; ++h) {
+          if (cnt[(size_t)h] > cap[(size_t)h]) { ++over; continue; }
+          tot += cnt[(size_t)h];
+          mx = std::max<int64_t>(mx, cnt[(size_t)h]);
+          big64 += cnt[(size_t)h] > 64;
+        }
+        fprintf(stderr, "[bias stats] candidates %lld (max %lld, rows > 64: %lld) overflowed rows %lld\n",
+                (long long)tot, (long long)mx, (long long)big64, (long long)over);
+      }
     }
     if (replace) {
       // CDF scratch = sum of degrees (the reference's temp tensor, :257-259): one D2H.
