@@ -1392,10 +1392,24 @@ __device__ __forceinline__ void stream_cand(const BiasHubArgs &a, global_ptr<flo
   key = v ? ares_key(a.cand.key[cb + e], pr[idx]) : -__builtin_inff();
 }
 
+// Writes row r's k picks (lane l < k: index idx_l) given its node-table entry and output offset.
+__device__ __forceinline__ void merge_emit_at(const BiasHubArgs &a, int64_t S, int64_t r,
+                                              const RowInfo &ri, int64_t out, int32_t idx_l,
+                                              int64_t k, int l) {
+  if (l < k) {
+    const int64_t v = as_global(ri.ptr)[idx_l];
+    a.rowpos[out + l] = r;
+    a.col[out + l] = v;
+    table_record(a.table, v, S + out + l);
+  }
+}
+
 // Emits each hub row's k picks from its candidate list (or recomputes the row when the list
 // overflowed).  Lists of at most 64: one half-wave per row.  Longer lists and recomputed rows:
 // one workgroup per row, 8 half-waves over interleaved 32-entry batches (or contiguous step
-// ranges), merged in LDS.
+// ranges), merged in LDS.  The loads are grouped by dependence level (the list's header and the
+// row's output slot together, both candidate batches together, the next batch's entries under
+// the current batch's probabilities): this pass is latency-bound.
 __device__ __forceinline__ void stream_merge_block(const BiasHubArgs &a, int64_t blk,
                                                    int64_t nblk) {
   __shared__ float s_key[8][32];
@@ -1407,18 +1421,23 @@ __device__ __forceinline__ void stream_merge_block(const BiasHubArgs &a, int64_t
   const int l = threadIdx.x & 31, g = threadIdx.x >> 5;
   for (int64_t h = blk * 8 + g; h < H; h += nblk * 8) {
     const int32_t n = a.cand.cnt[h], cap = a.cand.cap[h];
-    if (n > cap) continue;
-    if (n > 64) continue;
     const int64_t cb = a.cand.base[h];
     const global_ptr<float> pr = as_global(reinterpret_cast<const float *>(a.hub.aux[h]));
+    const int64_t r = a.hub.row[h];
+    if (n > cap || n > 64) continue;
+    const RowInfo ri = a.rowinfo[r];
+    const int64_t out = a.boff[r / kTileRows] + a.tpre[r];
+    const bool v0 = l < n, v1 = 32 + l < n;
+    const int32_t i0 = v0 ? a.cand.idx[cb + l] : INT32_MAX;
+    const int32_t i1 = v1 ? a.cand.idx[cb + 32 + l] : INT32_MAX;
+    const float u0 = v0 ? a.cand.key[cb + l] : 1.0f;
+    const float u1 = v1 ? a.cand.key[cb + 32 + l] : 1.0f;
+    const float p0 = v0 ? pr[i0] : 1.0f;
+    const float p1 = v1 ? pr[i1] : 1.0f;
     HalfTopK top;
-    for (int32_t b0 = 0; b0 < n; b0 += 32) {
-      float key;
-      int32_t idx;
-      stream_cand(a, pr, cb, n, b0 + l, key, idx);
-      top.push(key, idx, b0 + l < n, k, l);
-    }
-    merge_emit(a, S, h, top.bi, k, l);
+    top.push(v0 ? ares_key(u0, p0) : -__builtin_inff(), i0, v0, k, l);
+    if (n > 32) top.push(v1 ? ares_key(u1, p1) : -__builtin_inff(), i1, v1, k, l);
+    merge_emit_at(a, S, r, ri, out, top.bi, k, l);
   }
   for (int64_t h = blk; h < H; h += nblk) {
     const int32_t n = a.cand.cnt[h], cap = a.cand.cap[h];
@@ -1432,11 +1451,22 @@ __device__ __forceinline__ void stream_merge_block(const BiasHubArgs &a, int64_t
     } else {
       const int64_t cb = a.cand.base[h];
       const global_ptr<float> pr = as_global(reinterpret_cast<const float *>(a.hub.aux[h]));
+      int32_t e = 32 * g + l;
+      bool v = e < n;
+      int32_t idx = v ? a.cand.idx[cb + e] : INT32_MAX;
+      float u = v ? a.cand.key[cb + e] : 1.0f;
       for (int32_t b0 = 32 * g; b0 < n; b0 += 256) {
-        float key;
-        int32_t idx;
-        stream_cand(a, pr, cb, n, b0 + l, key, idx);
-        top.push(key, idx, b0 + l < n, k, l);
+        const float p = v ? pr[idx] : 1.0f;
+        // the next batch's entries load under this batch's probabilities and keys
+        const int32_t en = e + 256;
+        const bool vn = en < n;
+        const int32_t idxn = vn ? a.cand.idx[cb + en] : INT32_MAX;
+        const float un = vn ? a.cand.key[cb + en] : 1.0f;
+        top.push(v ? ares_key(u, p) : -__builtin_inff(), idx, v, k, l);
+        e = en;
+        v = vn;
+        idx = idxn;
+        u = un;
       }
     }
     tree_merge8(top, k, g, l, s_key, s_idx);
