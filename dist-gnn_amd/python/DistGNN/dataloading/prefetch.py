@@ -83,6 +83,8 @@ class PrefetchLoader:
         self._exhausted = False
         self._streams = _checkout_streams(self.device, depth)
         self._st = [s.cuda_stream for s in self._streams]
+        self._ids = [(s.stream_id, s.device_index, s.device_type) for s in self._streams]
+        self._c_raw, self._c_obj = None, None  # the caller's stream (cached torch object)
         self._dev = self.device.index
         self._inflight = collections.deque()
         self._n = 0
@@ -115,7 +117,7 @@ class PrefetchLoader:
         seeds.record_stream(self._streams[w])
         # int64 seeds (converted on C if need be) + one output buffer from B's pool
         prep = self.sampler._prepare(seeds, self.fan_out, packed=True,
-                                     alloc_stream=self._streams[w])
+                                     alloc_stream=self._ids[w])
         if prep[0] is not seeds:
             prep[0].record_stream(self._streams[w])
         # B waits for C (after the allocations), then the call is enqueued: one C-ABI call.
@@ -145,7 +147,9 @@ class PrefetchLoader:
             self.close()
             raise
         if buf is not None:  # the outputs' memory is used on C from here on
-            buf.record_stream(torch.cuda.current_stream(self.device))
+            if cur != self._c_raw:
+                self._c_raw, self._c_obj = cur, torch.cuda.current_stream(self.device)
+            buf.record_stream(self._c_obj)
         # C after B (the sample call); the feature and label gathers then run on C, whose
         # hardware queue the batch streams do not use -- the wait and both gathers in one
         # C-ABI call.  (The label gather depends on the seeds only; on C it stays off the
@@ -186,7 +190,7 @@ class PrefetchLoader:
         self._exhausted = True
         if self._streams:
             _return_streams(self.device, self._streams)
-            self._streams, self._st = [], []
+            self._streams, self._st, self._ids = [], [], []
 
     def __del__(self):
         try:

@@ -159,8 +159,9 @@ class P2PCacheSampler:
 
     def _prepare(self, seeds, fan_out, packed=False, alloc_stream=None):
         """packed: no per-hop pointer arrays (the buffer goes to the C ABI whole).
-        alloc_stream: a torch stream whose pool the output buffer comes from (the stream the
-        call writes it on; default the current stream)."""
+        alloc_stream: the (stream_id, device_index, device_type) of the torch stream whose pool
+        the output buffer comes from (the stream the call writes it on; default the current
+        stream)."""
         check_cuda(seeds, "seeds")
         s = seeds if seeds.dtype == torch.int64 and seeds.is_contiguous() else \
             as_i64(seeds, "seeds")
@@ -181,8 +182,15 @@ class P2PCacheSampler:
         if alloc_stream is None:
             buf = torch.empty(max(total, 1), dtype=torch.int64, device=s.device)
         else:
-            with torch.cuda.stream(alloc_stream):
+            # a bare current-stream switch around the allocation (the stream context manager
+            # costs several us of host time per batch, which a host-bound loader feels)
+            cur = _get_stream(s.device.index)
+            _set_stream(stream_id=alloc_stream[0], device_index=alloc_stream[1],
+                        device_type=alloc_stream[2])
+            try:
                 buf = torch.empty(max(total, 1), dtype=torch.int64, device=s.device)
+            finally:
+                _set_stream(stream_id=cur[0], device_index=cur[1], device_type=cur[2])
         return s, L, fo, caps, total, buf, None if packed else plan_ptrs(buf.data_ptr(), caps)
 
     def _views(self, seeds, buf, caps, total, sizes, L, cast=True):
@@ -308,6 +316,10 @@ class P2PCacheFeatureServer:
         if h is not None and h.value:
             lib.dgs_feature_server_destroy(h)
             self._h = None
+
+
+_get_stream = torch._C._cuda_getCurrentStream
+_set_stream = torch._C._cuda_setStream
 
 
 class _PendingSample:
