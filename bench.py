@@ -46,7 +46,8 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "dist-gnn_amd", "python"))
+# DGS_BENCH_PYDIR: another copy of the Python packages (same-box A/B of host-side changes)
+sys.path.insert(0, os.environ.get("DGS_BENCH_PYDIR", os.path.join(ROOT, "dist-gnn_amd", "python")))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

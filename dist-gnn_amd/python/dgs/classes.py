@@ -194,21 +194,19 @@ class P2PCacheSampler:
         return s, L, fo, caps, total, buf, None if packed else plan_ptrs(buf.data_ptr(), caps)
 
     def _views(self, seeds, buf, caps, total, sizes, L, cast=True):
-        # all views in one split: [U_h, pad, nnz_h, pad, nnz_h, pad] per hop
-        lens = []
-        for h, (f, e) in enumerate(caps):
-            U, nnz = sizes[3 * h + 1], sizes[3 * h + 2]
-            lens += (U, f - U, nnz, e - nnz, nnz, e - nnz)
-        if total == 0:
-            lens.append(1)
-        else:
-            lens.append(buf.numel() - total)
-        parts = buf.split(lens)
+        # per hop [frontier f | rows e | cols e]: the three live prefixes, by slicing (cheaper
+        # on the host than one split into every piece and pad)
         out = []
         cur = seeds
         cast = cast and self._id_dtype != torch.int64
+        off = 0
         for h in range(L):
-            fr, r, c = parts[6 * h], parts[6 * h + 2], parts[6 * h + 4]
+            f, e = caps[h]
+            U, nnz = sizes[3 * h + 1], sizes[3 * h + 2]
+            fr = buf[off:off + U]
+            r = buf[off + f:off + f + nnz]
+            c = buf[off + f + e:off + f + e + nnz]
+            off += f + 2 * e
             if cast:
                 fr, r, c = fr.to(self._id_dtype), r.to(self._id_dtype), c.to(self._id_dtype)
             out.append((cur, fr, r, c))
