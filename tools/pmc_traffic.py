@@ -14,7 +14,7 @@ import os
 import sys
 
 
-def per_kernel(path_glob, counter, kernel_re):
+def per_kernel(path_glob, counter, kernel_re, with_grid=False):
     import re
     vals = []
     for path in glob.glob(path_glob, recursive=True):
@@ -22,8 +22,26 @@ def per_kernel(path_glob, counter, kernel_re):
             if r.get("Counter_Name") != counter:
                 continue
             if re.search(kernel_re, r.get("Kernel_Name", "")):
-                vals.append(float(r["Counter_Value"]))
+                v = float(r["Counter_Value"])
+                vals.append((v, int(r.get("Grid_Size", 0) or 0)) if with_grid else v)
     return vals
+
+
+def rows_of_grid(grid_threads, row_bytes, vec=16, threads=64, unroll=4):
+    """Rows of one gather launch from its grid (one-wave workgroups, `unroll` 16-B chunks per
+    lane; the fused label workgroups, at most a few dozen, are within the rounding)."""
+    return max(1.0, grid_threads / threads * threads * unroll / (row_bytes / vec))
+
+
+def bench_side(fetch, write, row_bytes):
+    """Per-row HBM bytes over the bench's own gathers: launches whose grid says they gathered
+    more than 4x the median rows (the 2^20-row micro-benchmark in the same run) are left out."""
+    def per_row(vals):
+        rows = [rows_of_grid(g, row_bytes) for _, g in vals]
+        med = sorted(rows)[len(rows) // 2]
+        keep = [(v, r) for (v, _), r in zip(vals, rows) if r <= 4 * med]
+        return sum(v for v, _ in keep) * 1024 / sum(r for _, r in keep), len(keep), len(vals)
+    return per_row(fetch), per_row(write)
 
 
 def kernel_names(path_glob):
@@ -39,8 +57,10 @@ def main(root):
     # address-table form (TableSrc)
     table_re = r"k_gather<16, dgs::\(anonymous namespace\)::(TableSrc|StridedSrc<\w+>) ?>"
     plain_re = r"k_gather<16, dgs::\(anonymous namespace\)::PlainSrc<long> >"
-    bf = per_kernel(f"{root}/pmc_bench_fetch/**/*counter_collection.csv", "FETCH_SIZE", table_re)
-    bw = per_kernel(f"{root}/pmc_bench_write/**/*counter_collection.csv", "WRITE_SIZE", table_re)
+    bf = per_kernel(f"{root}/pmc_bench_fetch/**/*counter_collection.csv", "FETCH_SIZE", table_re,
+                    with_grid=True)
+    bw = per_kernel(f"{root}/pmc_bench_write/**/*counter_collection.csv", "WRITE_SIZE", table_re,
+                    with_grid=True)
     cf = per_kernel(f"{root}/pmc_calib_fetch/**/*counter_collection.csv", "FETCH_SIZE", plain_re)
     cw = per_kernel(f"{root}/pmc_calib_write/**/*counter_collection.csv", "WRITE_SIZE", plain_re)
     assert bf and bw and cf and cw, (len(bf), len(bw), len(cf), len(cw))
@@ -60,19 +80,25 @@ def main(root):
         for ln in open(line[0]):
             if ln.startswith("{"):
                 bench_rows = json.loads(ln)["gathered_rows_per_step"]
-    fetch = sum(bf) / len(bf) * 1024 * read_factor
-    write = sum(bw) / len(bw) * 1024 * write_factor
+    (rd_row, n_kept, n_all), (wr_row, _, _) = bench_side(bf, bw, D * 4)
+    rd_row *= read_factor
+    wr_row *= write_factor
+    fetch = rd_row * bench_rows if bench_rows else None
+    write = wr_row * bench_rows if bench_rows else None
     out = {
         "kernel": kernel_name, "dim": D,
         "calibration": {"workload": "sequential gather of 2^22 rows x 400 B (tools/gather_calib.py)",
                         "expected_read_bytes": calib_read, "fetch_size_bytes": cfetch,
                         "read_factor": read_factor, "expected_write_bytes": calib_write,
                         "write_size_bytes": cwrite, "write_factor": write_factor},
-        "bench_launches": len(bf),
+        "bench_launches": n_kept,
+        "launches_left_out": n_all - n_kept,
+        "rows_per_launch_source": "each launch's grid size (micro-benchmark launches left out)",
+        "hbm_read_bytes_per_row": rd_row, "hbm_write_bytes_per_row": wr_row,
         "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
-        "hbm_bytes_per_launch": fetch + write,
+        "hbm_bytes_per_launch": (fetch + write) if bench_rows else None,
         "rows_per_launch": bench_rows or None,
-        "hbm_bytes_per_row": (fetch + write) / bench_rows if bench_rows else None,
+        "hbm_bytes_per_row": rd_row + wr_row,
     }
     print(json.dumps(out, indent=1))
     return out
