@@ -139,7 +139,7 @@ class PrefetchLoader:
         pending, s64, w = self._inflight.popleft()
         st = self._st[w]
         cur = self._caller_stream()
-        buf = pending._buf
+        buf = pending.buffer
         try:
             blocks = pending.result(cast=False)
         except BaseException:

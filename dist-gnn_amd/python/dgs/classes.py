@@ -181,6 +181,11 @@ class P2PCacheSampler:
         # one allocation for every hop's (frontier, row, col) buffers
         if alloc_stream is None:
             buf = torch.empty(max(total, 1), dtype=torch.int64, device=s.device)
+        elif _set_stream is None or _get_stream is None:  # no bare stream switch in this build
+            with torch.cuda.stream(torch.cuda.Stream(stream_id=alloc_stream[0],
+                                                     device_index=alloc_stream[1],
+                                                     device_type=alloc_stream[2])):
+                buf = torch.empty(max(total, 1), dtype=torch.int64, device=s.device)
         else:
             # a bare current-stream switch around the allocation (the stream context manager
             # costs several us of host time per batch, which a host-bound loader feels)
@@ -316,8 +321,8 @@ class P2PCacheFeatureServer:
             self._h = None
 
 
-_get_stream = torch._C._cuda_getCurrentStream
-_set_stream = torch._C._cuda_setStream
+_get_stream = getattr(torch._C, "_cuda_getCurrentStream", None)
+_set_stream = getattr(torch._C, "_cuda_setStream", None)
 
 
 class _PendingSample:
@@ -328,6 +333,11 @@ class _PendingSample:
         self._owner, self._seeds, self._s64 = owner, seeds, s64
         self._L, self._caps, self._total, self._buf, self._stream = L, caps, total, buf, stream
         self._out = None
+
+    @property
+    def buffer(self):
+        """The call's output buffer until result() has built the views (then None)."""
+        return self._buf
 
     def result(self, cast=True):
         """cast=False leaves int32-id graphs' blocks as int64 (the caller casts them once its
