@@ -353,7 +353,8 @@ void Sampler::launch(Ctx &c, const Job &j, hipStream_t st) {
   const uint64_t *hop_seed = j.hop_seed.data();
   // device sizes: 3 per hop, then the bad-seed word (holds the seq of the last call that saw
   // a seed outside [0, num_nodes), or -seq of the last call whose relabel met a sampled id
-  // outside it (an internal error); zeroed at allocation, never reset)
+  // outside it (an out-of-range id in the graph's indices, or an internal error); zeroed at
+  // allocation, never reset)
   if (c.sizes.ensure(sizeof(int64_t) * (size_t)(3 * L + 1 + kSizesDbg)))
     DGS_HIP(hipMemsetAsync(c.sizes.p, 0, c.sizes.bytes, st));
   if (c.sizes_host.bytes < sizeof(int64_t) * (size_t)(3 * L + 2)) {
@@ -461,8 +462,9 @@ void Sampler::sample_end(int L, int64_t *sizes, hipStream_t st) {
   if (hsz[1 + 3 * L] < 0) {
     int64_t d[kSizesDbg] = {};
     (void)hipMemcpy(d, c.sizes.as<int64_t>() + 3 * L + 1, sizeof(d), hipMemcpyDeviceToHost);
-    DGS_CHECK(false, "sample: internal error: a sampled neighbour id was outside [0, num_nodes) "
-                         "(first: hop " + std::to_string(d[1]) + " edge " + std::to_string(d[2]) +
+    DGS_CHECK(false, "sample: a sampled neighbour id was outside [0, num_nodes): the graph's "
+                         "indices hold an id out of range, or an internal error (first: hop " +
+                         std::to_string(d[1]) + " edge " + std::to_string(d[2]) +
                          " id " + std::to_string(d[3]) + " nnz " + std::to_string(d[4]) +
                          " row " + std::to_string(d[5]) + ")");
   }

@@ -361,3 +361,27 @@ def test_prefetch_wide_gather_dropped_at_once(dgs):
             for u, v in zip(tg, te):
                 assert torch.equal(u, v)
             assert int(tg[3].min()) >= 0 if tg[3].numel() else True
+
+
+@pytest.mark.parametrize("bias", [False, True])
+def test_out_of_range_neighbour_id_raises(dgs, bias):
+    """A graph whose neighbour list holds an id outside [0, num_nodes) (the reference would read
+    out of bounds): the relabel pass range-checks every id it uses as a table index, keeps the
+    bad one out of the frontier and the call raises; the sampler stays usable afterwards (the
+    error is reported once per stream context: the flag is sticky, so a fresh sampler is used
+    for the check that follows)."""
+    n = 64
+    degs = [3] * n
+    indptr = torch.tensor([0] + list(torch.cumsum(torch.tensor(degs), 0)), dtype=torch.int64)
+    indices = torch.arange(int(indptr[-1]), dtype=torch.int64) % n
+    indices[1] = n + 5  # node 0's second neighbour
+    probs = torch.ones(indices.numel()) if bias else torch.Tensor()
+    sampler = dgs.classes.P2PCacheSampler(indptr, indices, probs, torch.arange(n), 0)
+    seeds = torch.tensor([0, 7], dtype=torch.int64, device="cuda")
+    with pytest.raises(RuntimeError, match="outside \\[0, num_nodes\\)"):
+        sampler._CAPI_sample_node_classifiction(seeds, [4, 4], False)
+    good = indices.clone()
+    good[1] = 1
+    ok = dgs.classes.P2PCacheSampler(indptr, good, probs, torch.arange(n), 0)
+    blocks = ok._CAPI_sample_node_classifiction(seeds, [4, 4], False)
+    assert int(blocks[0][1].max()) < n
