@@ -80,7 +80,7 @@ def parse(argv=None):
     p.add_argument("--mode", default="auto",
                    choices=["auto", "replicated", "hot-shard", "feature-shard", "shard"],
                    help="auto = replicated at N = 1, hot-shard at N > 1")
-    p.add_argument("--hot-frac", type=float, default=0.2,
+    p.add_argument("--hot-frac", type=float, default=0.5,
                    help="hot-shard: share of nodes (highest in-degree) cached on every GPU")
     p.add_argument("--shard", action="store_true", help="alias of --mode shard")
     p.add_argument("--bias", action="store_true",
