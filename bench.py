@@ -95,6 +95,10 @@ def parse(argv=None):
                    help="batches in flight (PrefetchLoader streams); 1 = the sequential loop")
     p.add_argument("--no-replicated-pass", action="store_true",
                    help="N > 1: skip the secondary replicated measurement")
+    p.add_argument("--no-xgmi-pass", action="store_true",
+                   help="N > 1: skip the secondary feature-shard (xGMI gather) measurement")
+    p.add_argument("--check-batches", type=int, default=4,
+                   help="N > 1: batches of the pre-timing self-check (0 = no check)")
     p.add_argument("--seq-calls", type=int, default=50,
                    help="synchronous calls timed for sequential_value (SURVEY 8(d): >= 50)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
@@ -369,7 +373,6 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
     import dgs
-    from DistGNN.dataloading import SeedGenerator
     if world > 1:
         # the library's setup collectives (IPC handles, cache lists, barriers); none in the
         # timed loop.  Every mode sets it up, so the secondary replicated pass is collective too.
@@ -425,18 +428,23 @@ def main():
     torch.cuda.synchronize()
     log(f"[bench] services ready in {time.time() - t0:.1f}s (mode {mode})")
     verify_setup(sampler, server, indices, feats, s_cache, f_cache, N, dev)
+    # N > 1: the replicated services (whole graph + features in this GPU's HBM) are the
+    # self-check's reference and the secondary `replicated` pass (collective constructors:
+    # every rank builds them in the same order)
+    everything = hot if hot is not None else torch.arange(N)
+    ref = None
+    if world > 1 and mode != "replicated":
+        ref = (dgs.classes.P2PCacheSampler(indptr, indices, probs, everything, dev_index),
+               dgs.classes.P2PCacheFeatureServer(feats, everything, dev_index))
+    self_check = None
+    if world > 1:
+        self_check = multi_rank_self_check(dgs, dist, sampler, server, ref, labels_dev, fan_out,
+                                           args, next_seeds_factory(train_local, args), rank,
+                                           world, dev, share)
     dgs.ops._CAPI_set_random_seed(args.seed + rank)
 
     torch.manual_seed(1)
-    loader = iter(SeedGenerator(train_local, args.batch, shuffle=True, drop_last=True))
-
-    def next_seeds():
-        nonlocal loader
-        try:
-            return next(loader)
-        except StopIteration:
-            loader = iter(SeedGenerator(train_local, args.batch, shuffle=True, drop_last=True))
-            return next(loader)
+    next_seeds = next_seeds_factory(train_local, args)
 
     elapsed, edges, rows, prof, step_gaps, mallocs = timed_pass(
         dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist, profile=True)
@@ -458,20 +466,22 @@ def main():
 
     # ---------------- N > 1: the same K steps with everything replicated (secondary figure)
     replicated = None
-    if world > 1 and mode != "replicated" and not args.no_replicated_pass:
-        del sampler, server  # collective destructors
-        torch.cuda.synchronize()
-        everything = hot if hot is not None else torch.arange(N)
-        sampler = dgs.classes.P2PCacheSampler(indptr, indices, probs, everything, dev_index)
-        server = dgs.classes.P2PCacheFeatureServer(feats, everything, dev_index)
+    if ref is not None and not args.no_replicated_pass:
         dgs.ops._CAPI_set_random_seed(args.seed + rank)
-        r_el, r_ed, _, _, _, _ = timed_pass(dgs, sampler, server, labels_dev, fan_out, args,
+        r_el, r_ed, _, _, _, _ = timed_pass(dgs, ref[0], ref[1], labels_dev, fan_out, args,
                                             next_seeds, dist, profile=False)
         r_el, r_ed = reduce_over_ranks(dist, red_dev, r_el, r_ed)
         replicated = {"value": r_ed / r_el, "unit": "sampled edges/s",
                       "ms_per_step": r_el * 1e3 / args.steps,
                       "workload": "whole graph + features in every GPU's HBM (configs[1] "
                                   "layout on every rank)"}
+
+    # ---------------- N > 1: configs[4]'s xGMI gather -- every feature row sharded v mod N
+    xgmi = None
+    if world > 1 and mode not in ("feature-shard", "shard") and not args.no_xgmi_pass:
+        xgmi = xgmi_pass(dgs, dist, ref[0] if ref is not None else sampler, feats, N, labels_dev,
+                         fan_out, args, next_seeds, rank, world, dev_index, red_dev, row_bytes,
+                         per_row)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -533,6 +543,13 @@ def main():
         "sequential_value": side["sequential_value"],
         "sequential_call_ms_median": side["seq_ms_median"],
         "replicated": replicated,
+        # N > 1: configs[4]'s gather + xGMI p2p layout (feature rows sharded v mod N, (N-1)/N of
+        # the gathered rows read from peers over xGMI), same sampler and batches
+        "xgmi_feature_shard": xgmi,
+        # N > 1: RCCL / host-transport all-gather of rank-dependent payloads and the first
+        # batches of this layout bit-exact against the replicated services (checked before the
+        # timed region; a mismatch ends the run non-zero on every rank)
+        "self_check": self_check,
         "host_step_gap_ms": step_gaps,
         "allocator_mallocs_in_timed_region": mallocs,
         "host_row_share": side["host_rows"],
@@ -586,14 +603,144 @@ def main():
         # links of XGMI_LINK_GBPS, so row reads are bounded by W * XGMI_LINK_GBPS per GPU;
         # the algorithmic bytes count each row twice (read + local write)
         out["roofline"]["xgmi_bound_GBps"] = 2 * world * XGMI_LINK_GBPS
-        out["roofline"]["frac_of_xgmi_bound"] = achieved / (2 * world * XGMI_LINK_GBPS)
+        out["roofline"]["frac_of_xgmi_bound"] = (None if share else
+                                                 achieved / (2 * world * XGMI_LINK_GBPS))
     if rank == 0:
         print(json.dumps(out), flush=True)
-    del sampler, server  # collective destructors (sharded mode) before the group goes away
+    # collective destructors (same order on every rank) before the group goes away
+    del ref
+    del sampler, server
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def next_seeds_factory(train_local, args):
+    """Endless SeedGenerator batches of this rank's train nids (shuffled, drop_last)."""
+    from DistGNN.dataloading import SeedGenerator
+    state = {"it": iter(SeedGenerator(train_local, args.batch, shuffle=True, drop_last=True))}
+
+    def next_seeds():
+        try:
+            return next(state["it"])
+        except StopIteration:
+            state["it"] = iter(SeedGenerator(train_local, args.batch, shuffle=True,
+                                             drop_last=True))
+            return next(state["it"])
+    return next_seeds
+
+
+def check_allgather(dgs, rank, world, dev):
+    """_Test_NCCLTensorAllGather (nccl_context.cc:52-112, the library's setup all-gather) with
+    rank-dependent lengths, as /root/reference/tests/test_nccl.py:14-21 does: rank r sends
+    3 + 5r int64 values r * 1000 + i; every rank checks every payload."""
+    mine = torch.arange(3 + 5 * rank, dtype=torch.int64, device=dev) + rank * 1000
+    got = dgs.ops._Test_NCCLTensorAllGather(mine)
+    if mine.is_cuda:
+        torch.cuda.synchronize()
+    bad = 0
+    for r in range(world):
+        want = torch.arange(3 + 5 * r, dtype=torch.int64) + r * 1000
+        bad += int(len(got) != world or not torch.equal(got[r].cpu(), want))
+    return bad
+
+
+def compare_batches(got, exp):
+    """Mismatching tensors between two lists of (blocks, x, y) batches (bit-exact)."""
+    bad = 0
+    for (gb, gx, gy), (eb, ex, ey) in zip(got, exp):
+        bad += int(len(gb) != len(eb))
+        for tg, te in zip(gb, eb):
+            bad += sum(int(u.dtype != v.dtype or not torch.equal(u, v)) for u, v in zip(tg, te))
+        bad += int(not torch.equal(gx, ex)) + int(not torch.equal(gy, ey))
+    return bad + abs(len(got) - len(exp))
+
+
+def multi_rank_self_check(dgs, dist, sampler, server, ref, labels_dev, fan_out, args,
+                          next_seeds, rank, world, dev, share):
+    """Before the timed region at N > 1: (a) the setup all-gather with rank-dependent payloads;
+    (b) --check-batches batches through this layout's services and PrefetchLoader, bit-exact
+    against the replicated services' sequential loop with the same launch seeds (the P2P
+    sampler and the peer-row gather draw the same RNG coordinates and copy the same rows,
+    rowwise_sampling_p2p.cu:38-39 = rowwise_sampling.cu:62-63).  A failure on any rank ends
+    every rank non-zero."""
+    from DistGNN.dataloading import PrefetchLoader
+    ag_bad = check_allgather(dgs, rank, world, dev)
+    batch_bad, n_check = 0, max(0, args.check_batches)
+    if n_check:
+        seeds = [next_seeds() for _ in range(n_check)]
+        rs, rf = ref if ref is not None else (sampler, server)
+        dgs.ops._CAPI_set_random_seed(4242 + rank)
+        exp = []
+        for sd in seeds:
+            blocks = rs._CAPI_sample_node_classifiction(sd, fan_out, False)
+            exp.append((blocks, rf._CAPI_get_feature(blocks[-1][1]),
+                        dgs.ops._CAPI_cuda_index_select(labels_dev, sd)))
+        dgs.ops._CAPI_set_random_seed(4242 + rank)
+        got = list(PrefetchLoader(sampler, seeds, fan_out, server=server, labels=labels_dev,
+                                  depth=args.depth))
+        torch.cuda.synchronize()
+        batch_bad = compare_batches(got, exp)
+        del got, exp
+    red = torch.device("cpu") if share else dev
+    t = torch.tensor([ag_bad, batch_bad], dtype=torch.int64, device=red)
+    dist.all_reduce(t)
+    ag_all, batch_all = int(t[0]), int(t[1])
+    res = {"allgather": "ok" if ag_all == 0 else f"{ag_all} bad payloads",
+           "batches_per_rank": n_check, "mismatched_tensors": batch_all,
+           "reference": "replicated services, sequential loop" if ref is not None
+           else "this layout's sequential loop", "ranks": world}
+    if ag_all or batch_all:
+        log(f"[bench] multi-rank self-check FAILED: {res}")
+        raise SystemExit(1)
+    log(f"[bench] multi-rank self-check ok: {res}")
+    return res
+
+
+def xgmi_pass(dgs, dist, sampler, feats, N, labels_dev, fan_out, args, next_seeds, rank, world,
+              dev_index, red_dev, row_bytes, per_row):
+    """configs[4]'s gather + xGMI p2p layout at N > 1: every feature row sharded v mod N behind
+    the P2P feature server (strided addressing, (N-1)/N of the gathered rows read one-sided from
+    peers over xGMI), the same K steps.  Checked bit-exact on --check-batches batches against a
+    local gather first.  Reports the gather kernel's rate against the xGMI bound."""
+    from DistGNN.dataloading import PrefetchLoader
+    fs = dgs.classes.P2PCacheFeatureServer(feats, torch.arange(rank, N, world), dev_index)
+    dev = labels_dev.device
+    bad = 0
+    for _ in range(max(1, args.check_batches)):
+        blocks = sampler._CAPI_sample_node_classifiction(next_seeds(), fan_out, False)
+        nids = blocks[-1][1]
+        bad += int(not torch.equal(fs._CAPI_get_feature(nids), feats[nids.cpu()].to(dev)))
+    remote = float((blocks[-1][1] % world != rank).double().mean())
+    dgs.ops._CAPI_set_random_seed(args.seed + rank)
+    el, ed, rows, prof, _, _ = timed_pass(dgs, sampler, fs, labels_dev, fan_out, args, next_seeds,
+                                          dist, profile=True)
+    g_ms = prof["gather_ms"] / max(prof["gather_launches"], 1)
+    achieved = rows * per_row / max(prof["gather_launches"], 1) / (g_ms * 1e-3) / 1e9 \
+        if g_ms > 0 else 0.0
+    el_all, ed_all, bad_all, ach_all = reduce_over_ranks(dist, red_dev, el, ed, bad, achieved)
+    del fs
+    torch.cuda.synchronize()
+    if bad_all:
+        log(f"[bench] xGMI feature-shard gather check FAILED on {int(bad_all)} batches")
+        raise SystemExit(1)
+    bound = 2 * world * XGMI_LINK_GBPS
+    shared = os.environ.get("DGS_BENCH_SHARE_DEVICE") == "1"
+    return {"mode": "feature-shard", "value": ed_all / el_all, "unit": "sampled edges/s",
+            "ms_per_step": el_all * 1e3 / args.steps, "layout": fs_layout_name(world),
+            "remote_row_share": remote, "checked_batches": max(1, args.check_batches),
+            "gather_GBps_per_gpu": ach_all / world, "avg_launch_ms": g_ms,
+            "xgmi_bound_GBps": bound,
+            # ranks sharing one GPU read their "peer" rows from the same HBM: no xGMI bound
+            "frac_of_xgmi_bound": None if shared else ach_all / world / bound,
+            "ranks_share_one_gpu": shared,
+            "frac_of_hbm": ach_all / world / HBM_PEAK_GBPS}
+
+
+def fs_layout_name(world):
+    return (f"feature rows v mod {world} over the GPUs (strided addressing), structure "
+            "replicated")
 
 
 def pmc_traffic(dim, rows_per_launch):

@@ -54,7 +54,9 @@ T *dev_ptr(T *p, const char *what) {
 
 // Device-memory check for the per-batch entry points, remembered per address: a caching
 // allocator hands the same few blocks back batch after batch, so the pointer query runs about
-// once per block (a host pointer fails here instead of faulting on the GPU later).
+// once per block (a host pointer fails here instead of faulting on the GPU later).  Best effort:
+// an address is not forgotten when its memory is freed, so a later allocation at a remembered
+// address skips the query (the cache is dropped every 4096 new addresses).
 void check_device_cached(const void *p, const char *what) {
   thread_local std::unordered_set<uintptr_t> seen;
   if (!p) throw Error(std::string(what) + " is null");
@@ -94,9 +96,10 @@ OpScratchLease op_scratch(hipStream_t st, HopScratch **ws) {
     p->last_use = ++tick;
     o = p;
     if (all.size() > kOpScratchMax) {
+      // only an entry of the current device: the synchronisation below covers its stream
       auto victim = all.end();
       for (auto it = all.begin(); it != all.end(); ++it)
-        if (it->second != o && it->second.use_count() == 1 &&
+        if (it->first.first == dev && it->second != o && it->second.use_count() == 1 &&
             (victim == all.end() || it->second->last_use < victim->second->last_use))
           victim = it;
       if (victim != all.end()) {
@@ -242,7 +245,7 @@ int dgs_loader_gather(dgs_sampler *s, dgs_feature_server *fs, void *producer, vo
                       void *label_out) {
   return guard([&] {
     if (s)
-      DGS_HIP(hipStreamWaitEvent(S(consumer), s->s->ended_event(S(producer)), 0));
+      s->s->wait_ended(S(producer), S(consumer));
     else
       stream_wait_impl(producer, consumer);
     const bool want_labels = labels && n_seeds > 0;
@@ -470,7 +473,8 @@ int dgs_sampler_sample_begin_after(dgs_sampler *s, void *wait_for, const int64_t
                                    int64_t *out, const uint64_t *launch_seeds, int flags,
                                    void *stream) {
   return guard([&] {
-    DGS_CHECK((flags & ~DGS_SAMPLE_HOST_ASYNC) == 0, "sample_begin: unknown flags");
+    DGS_CHECK((flags & ~(DGS_SAMPLE_HOST_ASYNC | DGS_SAMPLE_WAIT)) == 0,
+              "sample_begin: unknown flags");
     DGS_CHECK(L > 0 && L <= 64, "sample_begin: 1 to 64 hops");
     if (n_seeds > 0) check_device_cached(seeds, "seeds");
     check_device_cached(out, "out");
@@ -484,7 +488,11 @@ int dgs_sampler_sample_begin_after(dgs_sampler *s, void *wait_for, const int64_t
       cols[h] = p + fcap[h] + ecap[h];
       p += fcap[h] + 2 * ecap[h];
     }
-    if (wait_for) stream_wait_impl(wait_for, stream);
+    // DGS_SAMPLE_WAIT, not the handle, says whether to wait: NULL is the null stream (torch's
+    // default current stream), a producer like any other.  (Rounds 2-3 tested the handle, so a
+    // caller on the default stream got no wait at all -- round 4's root cause of the N = 2
+    // corruption: the loader's buffers came from that stream's pool.)
+    if (flags & DGS_SAMPLE_WAIT) stream_wait_impl(wait_for, stream);
     s->s->sample_begin(seeds, n_seeds, fan_out, L, replace != 0, fr, rows, cols, S(stream),
                        launch_seeds, (flags & DGS_SAMPLE_HOST_ASYNC) != 0);
   });
@@ -492,6 +500,10 @@ int dgs_sampler_sample_begin_after(dgs_sampler *s, void *wait_for, const int64_t
 
 int dgs_sampler_sample_end(dgs_sampler *s, int L, int64_t *sizes_out, void *stream) {
   return guard([&] { s->s->sample_end(L, sizes_out, S(stream)); });
+}
+
+int dgs_sampler_context_count(dgs_sampler *s, int64_t *n) {
+  return guard([&] { *n = (int64_t)s->s->num_contexts(); });
 }
 
 int dgs_sampler_local_cache(const dgs_sampler *s, const int64_t **sub_indptr, int64_t *n_rows,

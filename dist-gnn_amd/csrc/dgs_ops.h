@@ -132,7 +132,7 @@ void relabel_hop(const int64_t *seeds, Count S, const int64_t *col, const int64_
                  int64_t nnz_cap, bool seeds_unique, const Table &table, int64_t *unique,
                  int64_t *out_row, int64_t *out_col, int64_t *d_nunique, HopScratch &ws,
                  hipStream_t st, const HostSizes &pub = HostSizes{},
-                 RelabelTail *defer = nullptr);
+                 RelabelTail *defer = nullptr, const IdCheck &chk = IdCheck{});
 // launches a deferred relabel tail on its own
 void launch_relabel_tail(const RelabelTail &tail, hipStream_t st);
 

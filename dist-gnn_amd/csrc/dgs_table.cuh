@@ -27,6 +27,19 @@ struct Table {
 };
 
 
+// Range check of a sampler call's sampled ids (an out-of-range id in the graph's indices, or
+// an internal error).  The first failing element of the call stores bad_tag (-seq) to *bad,
+// a word the call's sizes are published with, and records {seq, hop, edge, id, nnz, row} in
+// dbg[0..5].  Tags carry the call's sequence number, so nothing needs resetting between calls
+// and a later call never reports an earlier call's error.
+struct IdCheck {
+  int64_t *bad = nullptr;
+  int64_t bad_tag = 0;
+  int64_t *dbg = nullptr;
+  uint64_t seq = 0;
+  int64_t hop = 0;
+};
+
 // The last pass of a hop's relabel (direct layout): out_col[e] = lab[col[e]] in place,
 // out_row[e] = lab[seeds[r]] when the seeds may repeat (else label(r) == r), then every touched
 // node's val returns to empty.  The touched nodes are exactly the hop's unique ids, so the reset
@@ -43,18 +56,30 @@ struct RelabelTail {
   const int64_t *unique;    // the hop's unique ids (first-occurrence order)
   const int64_t *d_nuniq;   // their count (device)
   int64_t nblk;  // 256-thread blocks covering S + nnz (upper bounds; >= nnz and >= U)
-  // an id outside [0, t.n) (never produced by a correct hop) stores bad_tag to *bad, if set
-  int64_t *bad = nullptr;
-  int64_t bad_tag = 0;
-  // diagnostics of the first such id: {taken, hop, edge, id, nnz, row}
-  int64_t *dbg = nullptr;
-  int64_t hop = 0;
+  // an id outside [0, t.n) (never produced by a correct hop) is reported here, if set; the
+  // hop's count pass (k_dcount) has already checked the same ids before the sizes were
+  // published, so this is the guard of the table indexing below
+  IdCheck chk;
 };
 
 #ifdef __HIPCC__
 // direct layout: node x's first position and label
 __device__ __forceinline__ int32_t *dval(const Table &t, int64_t x) { return t.val + 2 * x; }
 __device__ __forceinline__ int32_t *dlab(const Table &t, int64_t x) { return t.val + 2 * x + 1; }
+
+__device__ __forceinline__ void report_bad_id(const IdCheck &c, int64_t e, int64_t id,
+                                              int64_t nnz, int64_t row) {
+  if (!c.bad) return;
+  *c.bad = c.bad_tag;
+  if (c.dbg && atomicMax(reinterpret_cast<unsigned long long *>(c.dbg),
+                         (unsigned long long)c.seq) < (unsigned long long)c.seq) {
+    c.dbg[1] = c.hop;
+    c.dbg[2] = e;
+    c.dbg[3] = id;
+    c.dbg[4] = nnz;
+    c.dbg[5] = row;
+  }
+}
 
 // Ids are range-checked before they index the table (one compare each): a corrupt id yields -1
 // in the output instead of an address outside the table.
@@ -67,22 +92,14 @@ __device__ __forceinline__ void relabel_tail_block(const RelabelTail &r, int64_t
     const int64_t v = r.out_col[e];
     bool ok = (uint64_t)v < n;
     r.out_col[e] = ok ? *dlab(r.t, v) : -1;
+    int64_t row = -1;
     if (r.remap_rows) {
-      const int64_t row = r.out_row[e];
+      row = r.out_row[e];
       const int64_t x = (uint64_t)row < (uint64_t)r.Sc.get() ? r.seeds[row] : -1;
       ok &= (uint64_t)x < n;
       r.out_row[e] = (uint64_t)x < n ? *dlab(r.t, x) : -1;
     }
-    if (!ok && r.bad) {
-      *r.bad = r.bad_tag;
-      if (r.dbg && atomicCAS(reinterpret_cast<unsigned long long *>(r.dbg), 0ull, 1ull) == 0ull) {
-        r.dbg[1] = r.hop;
-        r.dbg[2] = e;
-        r.dbg[3] = v;
-        r.dbg[4] = nb;
-        r.dbg[5] = r.remap_rows ? r.out_row[e] : -1;
-      }
-    }
+    if (!ok) report_bad_id(r.chk, e, v, nb, row);
   }
   // (the label loads above read the other word of the pair: no conflict with the resets)
   if (e < nu) {

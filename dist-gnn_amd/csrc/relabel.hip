@@ -153,9 +153,12 @@ __device__ __forceinline__ int64_t first_flags(const int64_t *a, int64_t na, con
 
 // Pass 1 also leaves each thread's flags (one byte, bit j = element i0 + j) for pass 2, which
 // then needs no second round of random table reads.
+// It also range-checks the hop's sampled ids (and, at the first hop, each edge's seed row)
+// before the sizes are published, so a call sees its own out-of-range id (IdCheck).
 __global__ __launch_bounds__(kThreads) void k_dcount(const int64_t *a, Count nac,
                                                      const int64_t *b, const int64_t *d_nb,
-                                                     Table t, int64_t *tcnt, uint8_t *flags) {
+                                                     Table t, int64_t *tcnt, uint8_t *flags,
+                                                     IdCheck chk, const int64_t *rows) {
   latency_prio();
   __shared__ int64_t lds[kThreads / 64];
   const int64_t na = nac.get();
@@ -165,6 +168,16 @@ __global__ __launch_bounds__(kThreads) void k_dcount(const int64_t *a, Count nac
   int64_t x[kCompactItems];
   bool f[kCompactItems];
   const int64_t cnt = first_flags(a, na, b, n, t, i0, x, f);
+  if (chk.bad) {
+#pragma unroll
+    for (int j = 0; j < kCompactItems; ++j) {
+      const int64_t i = i0 + j;
+      if (i < na || i >= n) continue;
+      const int64_t row = rows ? rows[i - na] : 0;
+      if ((uint64_t)x[j] >= (uint64_t)t.n || (uint64_t)row >= (uint64_t)na)
+        report_bad_id(chk, i - na, x[j], n - na, rows ? row : -1);
+    }
+  }
   uint32_t fb = 0;
 #pragma unroll
   for (int j = 0; j < kCompactItems; ++j) fb |= (uint32_t)f[j] << j;
@@ -298,7 +311,8 @@ Table direct_table(DevBuf &pairs, int64_t num_nodes, bool *dirty, hipStream_t st
 void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64_t *d_nnz,
                  int64_t nnz_cap, bool seeds_unique, const Table &t, int64_t *unique,
                  int64_t *out_row, int64_t *out_col, int64_t *d_nunique, HopScratch &ws,
-                 hipStream_t st, const HostSizes &pub, RelabelTail *defer) {
+                 hipStream_t st, const HostSizes &pub, RelabelTail *defer,
+                 const IdCheck &chk) {
   const int64_t n_ub = Sc.v + nnz_cap;
   const int64_t nblk = ceil_div(n_ub > 0 ? n_ub : 1, kThreads);
   ws.misc.ensure(sizeof(int64_t) * (size_t)(2 * nblk + 2));
@@ -310,14 +324,15 @@ void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64
     ws.flags.ensure((size_t)(ntiles * kThreads));
     uint8_t *flags = ws.flags.as<uint8_t>();
     hipLaunchKernelGGL(k_dcount, dim3((unsigned)ntiles), dim3(kThreads), 0, st, seeds, Sc, col,
-                       d_nnz, t, tcnt, flags);
+                       d_nnz, t, tcnt, flags, chk,
+                       seeds_unique ? (const int64_t *)nullptr : (const int64_t *)out_row);
     DGS_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_dscatter, dim3((unsigned)ntiles), dim3(kThreads), 0, st, seeds, Sc,
                        col, d_nnz, t, (const int64_t *)tcnt, (const uint8_t *)flags, unique,
                        d_nunique, pub);
     DGS_LAUNCH_CHECK();
     const RelabelTail tail{seeds, Sc, d_nnz, t, (int)!seeds_unique, out_row, out_col,
-                           unique, d_nunique, nblk};
+                           unique, d_nunique, nblk, chk};
     if (defer) {
       *defer = tail;  // the caller launches it with the next hop's prep
     } else {

@@ -1561,9 +1561,21 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   const int64_t nworkers = (int64_t)bias_stream_blocks() * (kTileRows / 32);
   BiasCand cand{};
   if (bias_hubs) {
+    // Hub rows have degree > kBiasHubT and are distinct within a hop: at most
+    // min(S, E / kBiasHubT) of them, with at most E / kStreamChunk + S chunks.  The room is
+    // capped by a budget (DGS_BIAS_CAND_BUDGET entries, default 2^26 = 512 MB per context):
+    // rows past it get no room and are recomputed exactly (rare; correct either way).
+    const int64_t hubs_ub =
+        src.num_edges > 0 ? std::min<int64_t>(S, src.num_edges / kBiasHubT + 1) : S;
     const int64_t chunks =
-        src.num_edges > 0 ? src.num_edges / kStreamChunk + S : (int64_t(1) << 24);
-    int64_t limit = bias_room_start(S, chunks, k);
+        src.num_edges > 0 ? src.num_edges / kStreamChunk + hubs_ub : (int64_t(1) << 22);
+    static const int64_t budget = [] {
+      const char *e = getenv("DGS_BIAS_CAND_BUDGET");
+      const long long v = e ? atoll(e) : 0;
+      return v > 0 ? (int64_t)v : (int64_t(1) << 26);
+    }();
+    int64_t limit = bias_room_start(hubs_ub, chunks, k);
+    if (limit > budget) limit = budget;
     if (limit > INT32_MAX) limit = INT32_MAX;  // 32-bit list offsets (rows past it: recomputed)
     ws.cand.ensure(sizeof(int64_t) * (size_t)S + 2 * sizeof(int32_t) * (size_t)S +
                    (sizeof(float) + sizeof(int32_t)) * (size_t)limit);

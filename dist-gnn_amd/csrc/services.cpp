@@ -113,6 +113,8 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
   num_nodes_ = num_nodes;
   num_edges_ = num_edges;
   bias_ = probs != nullptr;
+  if (const char *e = std::getenv("DGS_SAMPLER_MAX_CTX"))
+    max_ctx_ = (size_t)std::max(1, std::atoi(e));
   hipStream_t st = nullptr;
   h_indptr_.attach(indptr, (num_nodes + 1) * 8);
   h_indices_.attach(indices, num_edges * 8);
@@ -167,21 +169,31 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
   src_.num_edges = num_edges;
 }
 
-Sampler::~Sampler() {
-  for (auto &kv : ctxs_) {
-    Ctx &c = *kv.second;
-    if (c.launcher.joinable()) {
-      {
-        std::lock_guard<std::mutex> g(c.mu);
-        c.stop = true;
-        c.stop_flag.store(true, std::memory_order_relaxed);
-      }
-      c.cv.notify_all();
-      c.launcher.join();
+// Stops a context's launcher thread and waits for its last call's kernels (the last relabel pass
+// may still run) before its buffers go.
+void Sampler::retire(Ctx &c) {
+  if (c.launcher.joinable()) {
+    {
+      std::lock_guard<std::mutex> g(c.mu);
+      c.stop = true;
+      c.stop_flag.store(true, std::memory_order_relaxed);
     }
-    if (c.seq > 0) (void)hipStreamSynchronize(c.stream);  // the last relabel pass may still run
-    if (c.end_ev) (void)hipEventDestroy(c.end_ev);
+    c.cv.notify_all();
+    c.launcher.join();
   }
+  if (c.seq > 0) {
+    if (c.end_ev)
+      (void)hipEventSynchronize(c.end_ev);
+    else
+      (void)hipStreamSynchronize(c.stream);
+  }
+  if (c.end_ev) (void)hipEventDestroy(c.end_ev);
+  c.end_ev = nullptr;
+}
+
+Sampler::~Sampler() {
+  for (auto &kv : ctxs_) retire(*kv.second);
+  ctxs_.clear();
   delete indptr_srv_;
   delete indices_srv_;
   delete probs_srv_;
@@ -209,14 +221,38 @@ void Sampler::bounds(int64_t n_seeds, const int64_t *fan_out, int L, int64_t *fc
   }
 }
 
-Sampler::Ctx &Sampler::ctx_for(hipStream_t st) {
-  std::lock_guard<std::mutex> g(ctx_mu_);
-  std::unique_ptr<Ctx> &c = ctxs_[st];
-  if (!c) {
-    c.reset(new Ctx);
-    c->stream = st;
+std::shared_ptr<Sampler::Ctx> Sampler::ctx_for(hipStream_t st) {
+  std::shared_ptr<Ctx> c, victim;
+  {
+    std::lock_guard<std::mutex> g(ctx_mu_);
+    std::shared_ptr<Ctx> &slot = ctxs_[st];
+    if (!slot) {
+      slot = std::make_shared<Ctx>();
+      slot->stream = st;
+    }
+    slot->last_use = ++ctx_tick_;
+    c = slot;
+    if (ctxs_.size() > max_ctx_) {
+      auto best = ctxs_.end();
+      for (auto it = ctxs_.begin(); it != ctxs_.end(); ++it) {
+        if (it->second == c || it->second.use_count() != 1) continue;  // held by a caller
+        std::unique_lock<std::mutex> lk(it->second->mu, std::try_to_lock);
+        if (!lk.owns_lock() || it->second->pending) continue;  // a call is outstanding
+        if (best == ctxs_.end() || it->second->last_use < best->second->last_use) best = it;
+      }
+      if (best != ctxs_.end()) {
+        victim = std::move(best->second);
+        ctxs_.erase(best);
+      }
+    }
   }
-  return *c;
+  if (victim) retire(*victim);  // no longer reachable: nothing else can hold it
+  return c;
+}
+
+size_t Sampler::num_contexts() {
+  std::lock_guard<std::mutex> g(ctx_mu_);
+  return ctxs_.size();
 }
 
 // sampler.cc:14-62, 146-166: hops run fan_out[L-1] .. fan_out[0]; seeds <- frontier.
@@ -232,8 +268,12 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
   sample_end(L, sizes, st);
 }
 
-// device words after the sizes and the bad-seed word: the relabel pass's diagnostics
-constexpr int kSizesDbg = 8;
+// Per-context device words, at fixed offsets whatever the call's hop count: the diagnostics of
+// the call's first out-of-range sampled id ({seq, hop, edge, id, nnz, row}, IdCheck), the
+// flag word, then 3 sizes per hop.  The flag word and the sizes are published together.
+constexpr int kDbgWords = 8;
+constexpr int kFlagWord = kDbgWords;
+constexpr int kSizes0 = kFlagWord + 1;
 
 // Enqueues every hop of one call on `st` and returns: the call's sizes are read by
 // sample_end.  One call per stream may be outstanding (its context holds the published sizes).
@@ -252,7 +292,8 @@ void Sampler::sample_begin(const int64_t *seeds, int64_t n_seeds, const int64_t 
   j.fr.assign(frontiers, frontiers + L);
   j.rows.assign(rows, rows + L);
   j.cols.assign(cols, cols + L);
-  Ctx &c = ctx_for(st);
+  const std::shared_ptr<Ctx> cp = ctx_for(st);
+  Ctx &c = *cp;
   std::unique_lock<std::mutex> lk(c.mu);
   DGS_CHECK(!c.pending, "sample: the previous call on this stream has not been ended");
   // One launch seed per hop (rowwise_sampling.cu:162), drawn together so that concurrent calls
@@ -351,12 +392,13 @@ void Sampler::launch(Ctx &c, const Job &j, hipStream_t st) {
   int64_t *const *rows = j.rows.data();
   int64_t *const *cols = j.cols.data();
   const uint64_t *hop_seed = j.hop_seed.data();
-  // device sizes: 3 per hop, then the bad-seed word (holds the seq of the last call that saw
-  // a seed outside [0, num_nodes), or -seq of the last call whose relabel met a sampled id
-  // outside it (an out-of-range id in the graph's indices, or an internal error); zeroed at
-  // allocation, never reset)
-  if (c.sizes.ensure(sizeof(int64_t) * (size_t)(3 * L + 1 + kSizesDbg)))
+  // Device words (kDbgWords diagnostics, the flag word, 3 sizes per hop; zeroed at allocation).
+  // The flag word holds seq when this call saw a seed outside [0, num_nodes) and -seq when one
+  // of its sampled ids was outside it (an out-of-range id in the graph's indices, or an internal
+  // error): tagged by the call, so it is never reset and never read for another call.
+  if (c.sizes.ensure(sizeof(int64_t) * (size_t)(kSizes0 + 3 * L)))
     DGS_HIP(hipMemsetAsync(c.sizes.p, 0, c.sizes.bytes, st));
+  // pinned host words: [0] publication sequence, [1] flag, [2 + 3h + i] sizes
   if (c.sizes_host.bytes < sizeof(int64_t) * (size_t)(3 * L + 2)) {
     c.sizes_host.flags = hipHostMallocCoherent | hipHostMallocMapped;
     c.sizes_host.ensure(sizeof(int64_t) * (size_t)(3 * L + 2));
@@ -365,11 +407,17 @@ void Sampler::launch(Ctx &c, const Job &j, hipStream_t st) {
                                     c.sizes_host.p, 0));
   }
   int64_t *dsz = c.sizes.as<int64_t>();
+  int64_t *dsizes = dsz + kSizes0;  // hop h: [3h + 1] unique count, [3h + 2] nnz
   // (the previous call on this stream may still be relabelling: stream order covers it)
   const uint64_t seq = ++c.seq;
   RowSrc src = src_;
-  src.bad = dsz + 3 * L;
+  src.bad = dsz + kFlagWord;
   src.bad_tag = (int64_t)seq;
+  IdCheck chk;
+  chk.bad = dsz + kFlagWord;
+  chk.bad_tag = -(int64_t)seq;
+  chk.dbg = dsz;
+  chk.seq = seq;
   std::vector<int64_t> fcap(L), ecap(L);
   bounds(n_seeds, fan_out, L, fcap.data(), ecap.data());
   const int64_t *cur = seeds;
@@ -384,8 +432,8 @@ void Sampler::launch(Ctx &c, const Job &j, hipStream_t st) {
     const int64_t k = fan_out[L - 1 - h];
     const uint64_t seed = hop_seed[h];
     const int64_t nnz_cap = ecap[h];
-    int64_t *d_nnz = dsz + 3 * h + 2;
-    int64_t *d_uniq = dsz + 3 * h + 1;
+    int64_t *d_nnz = dsizes + 3 * h + 2;
+    int64_t *d_uniq = dsizes + 3 * h + 1;
     const int tb = h & 1;
     const Table t = direct_table(c.dpair[tb], num_nodes_, &c.dirty[tb], st);
     c.dirty[tb] = true;
@@ -393,17 +441,15 @@ void Sampler::launch(Ctx &c, const Job &j, hipStream_t st) {
     sample_hop(src, cur, S, k, replace, bias_, seed, rows[h], cols[h], d_nnz, t, c.ws, st,
                have_tail ? &tail : nullptr);
     if (have_tail) c.dirty[tb ^ 1] = false;  // the previous hop's clean-up is enqueued
-    // the last hop's scatter publishes every size to pinned host memory (no copy, no sync)
+    // the last hop's scatter publishes the flag word and every size to pinned host memory (no
+    // copy, no sync); each hop's count pass range-checks its sampled ids before that, so the
+    // call sees its own flag
     const bool last = h == L - 1;
-    const HostSizes pub = last ? HostSizes{dsz, 3 * L + 1, c.sizes_host_dev, seq} : HostSizes{};
+    const HostSizes pub =
+        last ? HostSizes{dsz + kFlagWord, 3 * L + 1, c.sizes_host_dev, seq} : HostSizes{};
+    chk.hop = h;
     relabel_hop(cur, S, cols[h], d_nnz, nnz_cap, /*seeds_unique=*/h > 0, t, frontiers[h],
-                rows[h], cols[h], d_uniq, c.ws, st, pub, &tail);
-    tail.bad = src.bad;
-    tail.bad_tag = -(int64_t)seq;
-    tail.dbg = dsz + 3 * L + 1;
-    tail.hop = h;
-    // the last hop's pass runs after the sizes were published: its flag is seen by the
-    // stream's next call
+                rows[h], cols[h], d_uniq, c.ws, st, pub, &tail, chk);
     if (last) launch_relabel_tail(tail, st);
     have_tail = !last;
     if (last) c.dirty[tb] = false;
@@ -417,18 +463,20 @@ void Sampler::launch(Ctx &c, const Job &j, hipStream_t st) {
   DGS_HIP(hipEventRecord(c.end_ev, st));
 }
 
-hipEvent_t Sampler::ended_event(hipStream_t st) {
-  Ctx &c = ctx_for(st);
+void Sampler::wait_ended(hipStream_t st, hipStream_t consumer) {
+  const std::shared_ptr<Ctx> cp = ctx_for(st);
+  Ctx &c = *cp;
   std::lock_guard<std::mutex> g(c.mu);
-  DGS_CHECK(!c.pending && c.end_ev, "ended_event: no ended call on this stream");
-  return c.end_ev;
+  DGS_CHECK(!c.pending && c.end_ev, "wait_ended: no ended call on this stream");
+  DGS_HIP(hipStreamWaitEvent(consumer, c.end_ev, 0));
 }
 
 // Waits for the sizes of the call begun on `st` (published by its last scatter kernel): the
 // host returns while the last relabel pass still runs (every consumer of the outputs is
 // ordered after it on the stream).  A failed kernel shows up through hipStreamQuery.
 void Sampler::sample_end(int L, int64_t *sizes, hipStream_t st) {
-  Ctx &c = ctx_for(st);
+  const std::shared_ptr<Ctx> cp = ctx_for(st);
+  Ctx &c = *cp;
   std::unique_lock<std::mutex> lk(c.mu);
   DGS_CHECK(c.pending, "sample_end: no call outstanding on this stream");
   DGS_CHECK(L == c.pending_L, "sample_end: hop count differs from the call's");
@@ -457,11 +505,11 @@ void Sampler::sample_end(int L, int64_t *sizes, hipStream_t st) {
   }
   // A call with a bad seed fails after it has run (its rows were sampled as empty; the
   // reference reads out of bounds instead).
-  DGS_CHECK(hsz[1 + 3 * L] != (int64_t)seq,
-            "sample: a seed is outside [0, num_nodes)");
-  if (hsz[1 + 3 * L] < 0) {
-    int64_t d[kSizesDbg] = {};
-    (void)hipMemcpy(d, c.sizes.as<int64_t>() + 3 * L + 1, sizeof(d), hipMemcpyDeviceToHost);
+  const int64_t flag = hsz[1];
+  DGS_CHECK(flag != (int64_t)seq, "sample: a seed is outside [0, num_nodes)");
+  if (flag == -(int64_t)seq) {
+    int64_t d[kDbgWords] = {};
+    (void)hipMemcpy(d, c.sizes.as<int64_t>(), sizeof(d), hipMemcpyDeviceToHost);
     DGS_CHECK(false, "sample: a sampled neighbour id was outside [0, num_nodes): the graph's "
                          "indices hold an id out of range, or an internal error (first: hop " +
                          std::to_string(d[1]) + " edge " + std::to_string(d[2]) +
@@ -471,8 +519,8 @@ void Sampler::sample_end(int L, int64_t *sizes, hipStream_t st) {
   int64_t s = n_seeds;
   for (int h = 0; h < L; ++h) {
     sizes[3 * h + 0] = s;
-    sizes[3 * h + 1] = hsz[1 + 3 * h + 1];
-    sizes[3 * h + 2] = hsz[1 + 3 * h + 2];
+    sizes[3 * h + 1] = hsz[2 + 3 * h + 1];
+    sizes[3 * h + 2] = hsz[2 + 3 * h + 2];
     s = sizes[3 * h + 1];
   }
 }

@@ -78,10 +78,11 @@ class Sampler {
                     int64_t *const *cols, hipStream_t st, const uint64_t *launch_seeds,
                     bool host_async = false);
   void sample_end(int L, int64_t *sizes, hipStream_t st);
-  // The event the last call on `st` recorded after its launches (valid once that call has been
-  // ended and until the next call on `st` is begun): a consumer stream waits on it without a
-  // record of its own on the caller's thread.
-  hipEvent_t ended_event(hipStream_t st);
+  // `consumer` waits for the last call ended on `st`, on the event that call recorded after its
+  // launches (no event record on the caller's thread).
+  void wait_ended(hipStream_t st, hipStream_t consumer);
+  // sampling contexts currently held (one per stream that sampled recently; at most max_ctx)
+  size_t num_contexts();
   const int64_t *sub_indptr() const { return (const int64_t *)indptr_srv_->local(); }
   int64_t n_rows() const { return indptr_srv_->items(rank_) - 1; }
   const int64_t *sub_indices() const { return (const int64_t *)indices_srv_->local(); }
@@ -134,12 +135,22 @@ class Sampler {
     int pending_L = 0;
     int64_t pending_seeds = 0;
     hipEvent_t end_ev = nullptr;  // recorded on the stream after each call's launches
+    uint64_t last_use = 0;        // ctx_mu_ tick of the last lookup
   };
-  Ctx &ctx_for(hipStream_t st);
+  // The context of `st`, created on first use.  At most max_ctx_ are kept (DGS_SAMPLER_MAX_CTX,
+  // default 8): a new stream evicts the least recently used context that no thread holds and
+  // that has no call outstanding, after its last call's kernels have finished (its end event).
+  // A caller cycling through fresh streams therefore holds a bounded amount of HBM (each
+  // context holds relabel tables of 16 B per node plus scratch); the reference keeps no state
+  // between calls (sampler.cc:146-166).
+  std::shared_ptr<Ctx> ctx_for(hipStream_t st);
+  static void retire(Ctx &c);
   void launch(Ctx &c, const Job &j, hipStream_t st);
   void launcher_loop(Ctx &c, int dev);
   std::mutex ctx_mu_;
-  std::unordered_map<hipStream_t, std::unique_ptr<Ctx>> ctxs_;
+  std::unordered_map<hipStream_t, std::shared_ptr<Ctx>> ctxs_;
+  uint64_t ctx_tick_ = 0;
+  size_t max_ctx_ = 8;
 };
 
 class FeatureServer {

@@ -94,15 +94,15 @@ class PrefetchLoader:
             return _raw_stream(self._dev)
         return torch.cuda.current_stream(self.device).cuda_stream
 
-    # Stream ordering.  A batch's sample outputs are allocated from the pool of the batch stream
-    # B that writes them, and recorded on the caller's stream C when handed out: the caching
-    # allocator then reuses that memory only after both streams' uses (its own event queries).
-    # (Allocated on C instead, a block the previous batch's feature gather still writes -- x is
-    # dropped by the caller as soon as the gather is enqueued -- could be handed to the next
-    # batch, whose sampler would then race that gather unless B's wait for C held exactly;
-    # observed as feature bits in a batch's neighbour ids with two processes on one GPU.)
-    # B still waits for C before the launches (the seeds may be produced on C), and C waits
-    # for B before the outputs are used.
+    # Stream ordering.  B waits for C before the launches (the seeds may be produced on C; the
+    # wait is requested by a flag, since C is often the null stream, handle 0), and C waits for
+    # B before the outputs are used.  A batch's sample outputs are allocated from the pool of
+    # the batch stream B that writes them and recorded on C when handed out, so the caching
+    # allocator reuses that memory only after both streams' uses.  (Round 4 root cause of the
+    # round-3 N = 2 corruption: the C-ABI entry point skipped B's wait when C was the null
+    # stream, and rounds 2-3 allocated the outputs on C -- a later batch's buffer could be
+    # carved from an x whose feature gather was still queued on C, and that gather overwrote
+    # the sampler's output; tests/test_loader_order_gpu.py.)
     def _submit(self):
         try:
             seeds = next(self._seeds)

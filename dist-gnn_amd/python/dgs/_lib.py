@@ -72,6 +72,7 @@ _SIGS = {
                                                c_vp, ctypes.POINTER(c_u64), c_int, c_vp]),
     "dgs_loader_gather": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
                                   c_i64, c_vp]),
+    "dgs_sampler_context_count": (c_int, [c_vp, p_i64]),
     "dgs_sampler_local_cache": (c_int, [c_vp, p_vp, p_i64, p_vp, p_i64, p_vp]),
     "dgs_sampler_cache_map_size": (c_int, [c_vp, p_i64]),
     "dgs_sampler_cache_map_fill": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),

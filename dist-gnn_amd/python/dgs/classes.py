@@ -134,9 +134,11 @@ class P2PCacheSampler:
         if L and launch_seeds is not None:
             ls = (ctypes.c_uint64 * L)(*[int(x) & 0xFFFFFFFFFFFFFFFF for x in launch_seeds])
         if L and wait_for is not None:
+            # the wait is requested by the flag: wait_for may be 0, the null stream
             check(lib.dgs_sampler_sample_begin_after(self._h, wait_for, s.data_ptr(),
                                                      s.numel(), fo, L, int(bool(replace)),
-                                                     buf.data_ptr(), ls, 1 if host_async else 0,
+                                                     buf.data_ptr(), ls,
+                                                     _SAMPLE_WAIT | (1 if host_async else 0),
                                                      st))
         elif L:
             check(lib.dgs_sampler_sample_begin(self._h, c_vp(s.data_ptr()), s.numel(), fo, L,
@@ -217,6 +219,13 @@ class P2PCacheSampler:
             out.append((cur, fr, r, c))
             cur = fr
         return out
+
+    def _num_contexts(self):
+        """ADDITIVE (diagnostics): sampling contexts held, one per stream that sampled recently
+        (at most DGS_SAMPLER_MAX_CTX, default 8)."""
+        n = c_i64()
+        check(lib.dgs_sampler_context_count(self._h, ctypes.byref(n)))
+        return n.value
 
     def _CAPI_get_cpu_structure_tensors(self):
         indptr, indices, probs = self._cpu
@@ -321,6 +330,7 @@ class P2PCacheFeatureServer:
             self._h = None
 
 
+_SAMPLE_WAIT = 2  # DGS_SAMPLE_WAIT (include/dgs_amd.h)
 _get_stream = getattr(torch._C, "_cuda_getCurrentStream", None)
 _set_stream = getattr(torch._C, "_cuda_setStream", None)
 

@@ -188,14 +188,16 @@ int dgs_sampler_sample(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
  * _begin returns before they are enqueued; the caller then must not enqueue work on `stream`
  * until _end returns.  The output buffers and seeds must stay alive until _end. */
 #define DGS_SAMPLE_HOST_ASYNC 1
+#define DGS_SAMPLE_WAIT 2 /* dgs_sampler_sample_begin_after: wait for `wait_for` first */
 int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
                              const int64_t *fan_out, int L, int replace,
                              int64_t *const *frontiers, int64_t *const *rows,
                              int64_t *const *cols, const uint64_t *launch_seeds, int flags,
                              void *stream);
 int dgs_sampler_sample_end(dgs_sampler *s, int L, int64_t *sizes_out, void *stream);
-/* ADDITIVE: `stream` first waits for the work enqueued on `wait_for` so far (when non-NULL),
- * then dgs_sampler_sample_begin with every hop's outputs packed in one device buffer `out`:
+/* ADDITIVE: with DGS_SAMPLE_WAIT in `flags`, `stream` first waits for the work enqueued on
+ * `wait_for` so far (any stream, NULL = the null stream); then dgs_sampler_sample_begin with
+ * every hop's outputs packed in one device buffer `out`:
  * per hop h, frontier[fcap_h], rows[ecap_h], cols[ecap_h] back to back (the capacities of
  * dgs_sampler_bounds) -- one call per batch for a pipelined loader.  `seeds` must be device
  * memory (no pointer-attribute query); 1 <= L <= 64. */
@@ -203,13 +205,20 @@ int dgs_sampler_sample_begin_after(dgs_sampler *s, void *wait_for, const int64_t
                                    int64_t n_seeds, const int64_t *fan_out, int L, int replace,
                                    int64_t *out, const uint64_t *launch_seeds, int flags,
                                    void *stream);
+/* ADDITIVE (diagnostics): sampling contexts the sampler holds, one per stream that sampled
+ * recently.  At most DGS_SAMPLER_MAX_CTX (default 8) are kept: a new stream evicts the least
+ * recently used idle one (the reference keeps no per-stream state, sampler.cc:146-166). */
+int dgs_sampler_context_count(dgs_sampler *s, int64_t *n);
 /* _CAPI_get_local_cache_structure_tensors (sampler.cc:183-195): non-owning device views. */
 int dgs_sampler_local_cache(const dgs_sampler *s, const int64_t **sub_indptr, int64_t *n_rows,
                             const int64_t **sub_indices, int64_t *n_edges,
                             const float **sub_probs);
 /* _CAPI_get_local_cache_hashmap_tensors (sampler.cc:197-201): the (nid, row, device) map of
  * every cached node, local entries taking priority (hashmap.cu:37-72).  Two-step: query
- * the count, then fill caller buffers (device). */
+ * the count, then fill caller buffers (device).  SHAPE DEVIATION: the reference returns its
+ * open-addressing table arrays (capacity 2 * UpPow(total cached), empty slots included,
+ * hashmap.cu:20, sampler.cc:192-196); this returns one entry per cached node, in node-id order,
+ * no empty slots -- the same lookup results. */
 int dgs_sampler_cache_map_size(const dgs_sampler *s, int64_t *n);
 int dgs_sampler_cache_map_fill(const dgs_sampler *s, int64_t *key, int64_t *idx,
                                int64_t *devid, void *stream);
@@ -250,12 +259,13 @@ int dgs_feature_server_destroy(dgs_feature_server *s);
 
 /* ------------------------------------------------------------------------------------
  * Instrumentation (bench.py).  `mask` selects what is timed: DGS_PROFILE_GATHER = feature-
- * server gather kernels, DGS_PROFILE_SELECT = index_select kernels (both launched with
- * hipExtLaunchKernelGGL start/stop events, recorded by the GPU at the kernel's own start and
- * end on the stream it runs on), DGS_PROFILE_SAMPLE = whole sample calls (one stream event
- * before the first and one after the last kernel).  0 disables; any nonzero value outside the
- * three bits enables all.  dgs_profile_read() returns the summed milliseconds and counts, then
- * resets them.
+ * server gather kernels, DGS_PROFILE_SELECT = index_select kernels (both timed by the kernel
+ * itself: the first wave of every workgroup stamps s_memrealtime, the 100 MHz device wall
+ * clock, at its start and after its last store; a launch's time is its last end - first start,
+ * read back from a stamp slab reserved when profiling is switched on), DGS_PROFILE_SAMPLE =
+ * whole sample calls (one stream event before the first and one after the last kernel).
+ * 0 disables; any nonzero value outside the three bits enables all.  dgs_profile_read()
+ * returns the summed milliseconds and counts, then resets them.
  * ---------------------------------------------------------------------------------- */
 #define DGS_PROFILE_GATHER 1
 #define DGS_PROFILE_SAMPLE 2

@@ -114,3 +114,63 @@ def test_shared_inputs_one_host_copy(tmp_path):
     deg = torch.bincount(r0["indices"], minlength=n)
     assert torch.equal(r0["probs"], (1 + deg[r0["indices"]]).float())
     assert not glob.glob(f"/dev/shm/dgs_bench_test{port}_*")
+
+
+def _selfcheck_worker(rank, world, port, corrupt, out):
+    """bench.multi_rank_self_check's all-gather leg and cross-rank verdict, with the library's
+    all-gather stood in by a gloo one (optionally corrupting one payload on rank 1)."""
+    import types
+
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allgather(t):
+        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([t.numel()]))
+        m = max(int(x) for x in sizes)
+        pad = torch.zeros(m, dtype=t.dtype)
+        pad[:t.numel()] = t
+        outs = [torch.empty(m, dtype=t.dtype) for _ in range(world)]
+        dist.all_gather(outs, pad)
+        res = [o[:int(n)] for o, n in zip(outs, sizes)]
+        if corrupt and rank == 1:
+            res[0] = res[0] + 1
+        return res
+
+    fake = types.SimpleNamespace(ops=types.SimpleNamespace(_Test_NCCLTensorAllGather=allgather))
+    args = bench.parse(["--check-batches", "0"])
+    try:
+        res = bench.multi_rank_self_check(fake, dist, None, None, None, None, [5], args, None,
+                                          rank, world, torch.device("cpu"), True)
+        verdict = res["allgather"]
+    except SystemExit as e:
+        verdict = f"exit {e.code}"
+    with open(f"{out}/r{rank}.txt", "w") as f:
+        f.write(verdict)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_multi_rank_self_check_verdict(tmp_path, corrupt):
+    """Rank-dependent payload lengths all-gathered and checked on every rank; one bad payload
+    on one rank makes every rank exit non-zero (the verdict is all-reduced)."""
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_selfcheck_worker, args=(2, port, corrupt, str(tmp_path)), nprocs=2, join=True)
+    got = [open(tmp_path / f"r{r}.txt").read() for r in range(2)]
+    assert got == (["exit 1", "exit 1"] if corrupt else ["ok", "ok"])
+
+
+def test_compare_batches_counts_mismatches():
+    b = [(torch.arange(3), torch.arange(5), torch.arange(4), torch.arange(4))]
+    x, y = torch.ones(5, 2), torch.arange(3)
+    good = [(b, x, y)]
+    assert bench.compare_batches(good, [(b, x.clone(), y.clone())]) == 0
+    b2 = [(torch.arange(3), torch.arange(5), torch.arange(4), torch.tensor([0, 1, 2, 4]))]
+    assert bench.compare_batches(good, [(b2, x, y)]) == 1
+    assert bench.compare_batches(good, [(b, x + 1, y)]) == 1
+    assert bench.compare_batches(good, []) == 1

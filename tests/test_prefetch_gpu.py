@@ -363,25 +363,85 @@ def test_prefetch_wide_gather_dropped_at_once(dgs):
             assert int(tg[3].min()) >= 0 if tg[3].numel() else True
 
 
-@pytest.mark.parametrize("bias", [False, True])
-def test_out_of_range_neighbour_id_raises(dgs, bias):
-    """A graph whose neighbour list holds an id outside [0, num_nodes) (the reference would read
-    out of bounds): the relabel pass range-checks every id it uses as a table index, keeps the
-    bad one out of the frontier and the call raises; the sampler stays usable afterwards (the
-    error is reported once per stream context: the flag is sticky, so a fresh sampler is used
-    for the check that follows)."""
+def _bad_id_graph(dgs, bias):
+    """64 nodes of degree 3, node v -> (3v, 3v+1, 3v+2) mod 64, except that node 0's second
+    neighbour is 69 (outside [0, 64): the reference would read out of bounds).  Seed 0 meets it
+    at the first hop; seed 21 (neighbours 63, 0, 1) only at the second."""
     n = 64
-    degs = [3] * n
-    indptr = torch.tensor([0] + list(torch.cumsum(torch.tensor(degs), 0)), dtype=torch.int64)
-    indices = torch.arange(int(indptr[-1]), dtype=torch.int64) % n
-    indices[1] = n + 5  # node 0's second neighbour
+    indptr = torch.arange(0, 3 * n + 1, 3, dtype=torch.int64)
+    indices = torch.arange(3 * n, dtype=torch.int64) % n
+    indices[1] = n + 5
     probs = torch.ones(indices.numel()) if bias else torch.Tensor()
-    sampler = dgs.classes.P2PCacheSampler(indptr, indices, probs, torch.arange(n), 0)
-    seeds = torch.tensor([0, 7], dtype=torch.int64, device="cuda")
-    with pytest.raises(RuntimeError, match="outside \\[0, num_nodes\\)"):
-        sampler._CAPI_sample_node_classifiction(seeds, [4, 4], False)
-    good = indices.clone()
-    good[1] = 1
-    ok = dgs.classes.P2PCacheSampler(indptr, good, probs, torch.arange(n), 0)
-    blocks = ok._CAPI_sample_node_classifiction(seeds, [4, 4], False)
+    return dgs.classes.P2PCacheSampler(indptr, indices, probs, torch.arange(n), 0), n
+
+
+@pytest.mark.parametrize("bias", [False, True])
+@pytest.mark.parametrize("case", ["first_hop", "last_hop_of_one", "last_hop_of_two",
+                                  "middle_hop"])
+def test_out_of_range_neighbour_id_raises(dgs, bias, case):
+    """A sampled neighbour id outside [0, num_nodes) makes the call that sampled it raise --
+    also when it is first met at the call's last hop (each hop's count pass checks the ids
+    before the sizes are published) -- with the hop that met it; the id stays out of the
+    frontier, and the same sampler's next call, which does not reach it, returns normally
+    (the flag is tagged by call: nothing sticks to the stream context)."""
+    sampler, n = _bad_id_graph(dgs, bias)
+    seeds, fan_out, hop = {"first_hop": ([0, 7], [4, 4], 0),
+                           "last_hop_of_one": ([0, 7], [4], 0),
+                           "last_hop_of_two": ([21], [4, 4], 1),
+                           "middle_hop": ([21], [4, 4, 4], 1)}[case]
+    s = torch.tensor(seeds, dtype=torch.int64, device="cuda")
+    with pytest.raises(RuntimeError, match=f"outside \\[0, num_nodes\\).*hop {hop} .*id {n + 5}"):
+        sampler._CAPI_sample_node_classifiction(s, fan_out, False)
+    for _ in range(2):  # usable afterwards, on the same stream context
+        blocks = sampler._CAPI_sample_node_classifiction(
+            torch.tensor([9, 10], dtype=torch.int64, device="cuda"), fan_out, False)
+        assert int(blocks[-1][1].max()) < n and int(blocks[-1][3].min()) >= 0
+
+
+def test_out_of_range_id_raises_in_its_own_batch(dgs):
+    """Pipelined: the batch whose last hop meets the bad id raises when it is handed out, not a
+    later batch (round 3: the last hop's flag surfaced at the stream's next call)."""
+    from DistGNN.dataloading import PrefetchLoader
+    sampler, n = _bad_id_graph(dgs, False)
+    mk = lambda ids: torch.tensor(ids, dtype=torch.int64, device="cuda")  # noqa: E731
+    ld = iter(PrefetchLoader(sampler, [mk([9]), mk([0, 7]), mk([10]), mk([11])], [4], depth=3))
+    blocks, _, _ = next(ld)
     assert int(blocks[0][1].max()) < n
+    with pytest.raises(RuntimeError, match="outside \\[0, num_nodes\\)"):
+        next(ld)
+
+
+def test_sampler_contexts_are_bounded(dgs):
+    """A caller that samples under 32 fresh streams (e.g. a new torch.cuda.Stream per call):
+    the sampler keeps at most 8 per-stream contexts (the least recently used idle one is evicted
+    after its last kernels finished), device memory stays bounded, and every call on every
+    stream is bit-exact against the same call on the default stream."""
+    from DistGNN.dataloading.synthetic import rmat_csc_numpy
+    indptr, indices = rmat_csc_numpy(20, 4, seed=5)  # 2^20 nodes: 16 MB of relabel tables
+    sampler = dgs.classes.P2PCacheSampler(torch.from_numpy(indptr), torch.from_numpy(indices),
+                                          torch.Tensor(), torch.arange(indptr.size - 1), 0)
+    fan_out, ls = [15, 10, 5], [11, 22, 33]
+    seeds = torch.randint(0, indptr.size - 1, (512,), generator=torch.Generator().manual_seed(1))
+    seeds = seeds.cuda()
+    exp = sampler._sample_seeded(seeds, fan_out, False, ls)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free0 = torch.cuda.mem_get_info()[0]
+    per_ctx = None
+    streams = [torch.cuda.Stream() for _ in range(32)]
+    assert len({s.cuda_stream for s in streams}) == 32
+    for i, st in enumerate(streams):
+        with torch.cuda.stream(st):
+            got = sampler._sample_seeded(seeds, fan_out, False, ls)
+            for tg, te in zip(got, exp):
+                for u, v in zip(tg, te):
+                    assert torch.equal(u, v)
+        del got
+        torch.cuda.synchronize()
+        if i == 0:
+            torch.cuda.empty_cache()
+            per_ctx = free0 - torch.cuda.mem_get_info()[0]
+        assert sampler._num_contexts() <= 8
+    torch.cuda.empty_cache()
+    grown = free0 - torch.cuda.mem_get_info()[0]
+    assert per_ctx > 0 and grown <= 10 * per_ctx, (grown, per_ctx)
