@@ -50,15 +50,17 @@ def main():
             d = json.loads(line)
             iso = d.get("roofline_isolated", {}).get("frac", 0.0)
             res[lib].append((d["ms_per_step"], d["sample_span_ms_per_call"],
-                             d["roofline"]["frac"], iso, d["value"]))
+                             d["roofline"]["frac"], iso, d["value"],
+                             d.get("sequential_value", 0.0)))
             print(f"round {r} {lib}: {d['ms_per_step'] * 1e3:.1f} us/step "
                   f"sample span {d['sample_span_ms_per_call'] * 1e3:.1f} us "
-                  f"gather frac {d['roofline']['frac']:.3f} (isolated {iso:.3f})", flush=True)
+                  f"gather frac {d['roofline']['frac']:.3f} (isolated {iso:.3f}) "
+                  f"sequential {d.get('sequential_value', 0.0) / 1e6:.0f} M", flush=True)
     for lib, v in res.items():
-        med = [statistics.median(x[i] for x in v) for i in range(5)]
+        med = [statistics.median(x[i] for x in v) for i in range(6)]
         print(f"MEDIAN {lib}: {med[4] / 1e6:.0f} M edges/s, {med[0] * 1e3:.1f} us/step, "
               f"sample span {med[1] * 1e3:.1f} us, gather frac {med[2]:.3f}, "
-              f"isolated {med[3]:.3f}")
+              f"isolated {med[3]:.3f}, sequential {med[5] / 1e6:.0f} M edges/s")
 
 
 if __name__ == "__main__":

@@ -24,5 +24,11 @@ for n, d in sorted(agg.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
         line += f" SALU/wave={d.get('SQ_INSTS_SALU', 0) / c / waves:7.0f}"
         line += f" LDS/wave={d.get('SQ_INSTS_LDS', 0) / c / waves:6.0f}"
     if d.get("SQ_WAVE_CYCLES"):
-        line += f" VALU-active/wave-cycles={d.get('SQ_ACTIVE_INST_VALU', 0) / d['SQ_WAVE_CYCLES']:.3f}"
+        wc = d["SQ_WAVE_CYCLES"]
+        line += f" VALU-active/wave-cycles={d.get('SQ_ACTIVE_INST_VALU', 0) / wc:.3f}"
+        if waves:
+            line += f" wave-cycles/wave={wc / c / waves:8.0f}"
+        for k in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY"):
+            if k in d:
+                line += f" {k[3:].lower()}/wave-cycles={d[k] / wc:.3f}"
     print(line)

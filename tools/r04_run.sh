@@ -48,6 +48,33 @@ for step in "$@"; do
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py \
         --no-cpu-baseline > $O/bench_rocprof.json 2> $O/bench_rocprof.err; rc=$?
       cut -c1-200 $O/bench_rocprof.json; ok $rc ;;
+    ab)
+      # same-box A/B: AB_VARIANTS (space-separated ab_bench variants), AB_ARGS (bench args)
+      timeout -k 10 1000 python tools/ab_bench.py --rounds ${AB_ROUNDS:-3} -- $AB_VARIANTS \
+        -- ${AB_ARGS:-} > $O/ab.txt 2>&1; rc=$?; grep MEDIAN $O/ab.txt; ok $rc ;;
+    synchost)
+      timeout -k 10 300 python tools/r04_sync_host.py > $O/sync_host.txt 2>&1; rc=$?
+      cat $O/sync_host.txt | tail -12; ok $rc ;;
+    pmcpipe)
+      # SQ counters per kernel, pipelined (depth 3) and sequential (depth 1) uniform loops
+      export TMPDIR=/tmp
+      for d in 3 1; do
+        timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU \
+          SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_SALU \
+          --output-format csv -d $O/pmc_d$d -- python3 bench.py --depth $d --steps 200 \
+          --warmup 10 --seq-calls 3 --no-cpu-baseline > $O/pmc_d$d.log 2>&1; rc=$?
+        ok $rc
+        python3 tools/pmc_kernels.py "$(find $O/pmc_d$d -name '*counter_collection.csv' | head -n 1)" \
+          > $O/pmc_d${d}_summary.txt; head -12 $O/pmc_d${d}_summary.txt | cut -c1-250
+      done ;;
+    calltrace)
+      # kernel trace of the sequential loop: one sample call's kernels in stream order
+      export TMPDIR=/tmp
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/calls -- \
+        python3 bench.py --depth 1 --steps 100 --warmup 10 --seq-calls 3 --no-cpu-baseline \
+        ${CALL_ARGS:-} > $O/calls.log 2>&1; rc=$?; ok $rc
+      python3 tools/call_breakdown.py "$(ls -t $(find $O/calls -name '*kernel_trace.csv') | head -n 1)" \
+        > $O/call_breakdown.txt; cat $O/call_breakdown.txt | tail -25 ;;
     *) echo "unknown step $step" ;;
   esac
 done
