@@ -239,6 +239,13 @@ int dgs_stream_wait(void *producer, void *consumer) {
   return guard([&] { stream_wait_impl(producer, consumer); });
 }
 
+int dgs_stream_wait_event(void *event, void *consumer) {
+  return guard([&] {
+    DGS_CHECK(event, "stream_wait_event: null event");
+    DGS_HIP(hipStreamWaitEvent(S(consumer), reinterpret_cast<hipEvent_t>(event), 0));
+  });
+}
+
 int dgs_loader_gather(dgs_sampler *s, dgs_feature_server *fs, void *producer, void *consumer,
                       const int64_t *nids, int64_t n, void *feat_out, const void *labels,
                       int64_t label_row_bytes, const int64_t *seeds, int64_t n_seeds,
@@ -468,31 +475,57 @@ int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_see
   });
 }
 
+// Per-hop pointers into a packed output buffer (frontier[fcap], rows[ecap], cols[ecap] per hop).
+static void packed_ptrs(const Sampler &smp, int64_t n_seeds, const int64_t *fan_out, int L,
+                        int64_t *out, int64_t **fr, int64_t **rows, int64_t **cols) {
+  int64_t fcap[64], ecap[64];
+  smp.bounds(n_seeds, fan_out, L, fcap, ecap);
+  int64_t *p = out;
+  for (int h = 0; h < L; ++h) {
+    fr[h] = p;
+    rows[h] = p + fcap[h];
+    cols[h] = p + fcap[h] + ecap[h];
+    p += fcap[h] + 2 * ecap[h];
+  }
+}
+
+int dgs_sampler_sample_packed(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
+                              const int64_t *fan_out, int L, int replace, int64_t *out,
+                              int64_t *sizes_out, void *stream) {
+  return guard([&] {
+    DGS_CHECK(L > 0 && L <= 64, "sample: 1 to 64 hops");
+    if (n_seeds > 0) check_device_cached(seeds, "seeds");
+    check_device_cached(out, "out");
+    int64_t *fr[64], *rows[64], *cols[64];
+    packed_ptrs(*s->s, n_seeds, fan_out, L, out, fr, rows, cols);
+    s->s->sample(seeds, n_seeds, fan_out, L, replace != 0, fr, rows, cols, sizes_out, S(stream));
+  });
+}
+
 int dgs_sampler_sample_begin_after(dgs_sampler *s, void *wait_for, const int64_t *seeds,
                                    int64_t n_seeds, const int64_t *fan_out, int L, int replace,
                                    int64_t *out, const uint64_t *launch_seeds, int flags,
                                    void *stream) {
   return guard([&] {
-    DGS_CHECK((flags & ~(DGS_SAMPLE_HOST_ASYNC | DGS_SAMPLE_WAIT)) == 0,
+    DGS_CHECK((flags & ~(DGS_SAMPLE_HOST_ASYNC | DGS_SAMPLE_WAIT | DGS_SAMPLE_WAIT_EVENT)) == 0,
               "sample_begin: unknown flags");
+    DGS_CHECK(!((flags & DGS_SAMPLE_WAIT) && (flags & DGS_SAMPLE_WAIT_EVENT)),
+              "sample_begin: DGS_SAMPLE_WAIT and DGS_SAMPLE_WAIT_EVENT exclude each other");
+    DGS_CHECK(!(flags & DGS_SAMPLE_WAIT_EVENT) || wait_for,
+              "sample_begin: DGS_SAMPLE_WAIT_EVENT needs an event");
     DGS_CHECK(L > 0 && L <= 64, "sample_begin: 1 to 64 hops");
     if (n_seeds > 0) check_device_cached(seeds, "seeds");
     check_device_cached(out, "out");
-    int64_t fcap[64], ecap[64];
     int64_t *fr[64], *rows[64], *cols[64];
-    s->s->bounds(n_seeds, fan_out, L, fcap, ecap);
-    int64_t *p = out;  // per hop: frontier[fcap], rows[ecap], cols[ecap]
-    for (int h = 0; h < L; ++h) {
-      fr[h] = p;
-      rows[h] = p + fcap[h];
-      cols[h] = p + fcap[h] + ecap[h];
-      p += fcap[h] + 2 * ecap[h];
-    }
+    packed_ptrs(*s->s, n_seeds, fan_out, L, out, fr, rows, cols);
     // DGS_SAMPLE_WAIT, not the handle, says whether to wait: NULL is the null stream (torch's
     // default current stream), a producer like any other.  (Rounds 2-3 tested the handle, so a
     // caller on the default stream got no wait at all -- round 4's root cause of the N = 2
     // corruption: the loader's buffers came from that stream's pool.)
     if (flags & DGS_SAMPLE_WAIT) stream_wait_impl(wait_for, stream);
+    // or on an event the caller recorded earlier (where its seeds were complete)
+    if (flags & DGS_SAMPLE_WAIT_EVENT)
+      DGS_HIP(hipStreamWaitEvent(S(stream), reinterpret_cast<hipEvent_t>(wait_for), 0));
     s->s->sample_begin(seeds, n_seeds, fan_out, L, replace != 0, fr, rows, cols, S(stream),
                        launch_seeds, (flags & DGS_SAMPLE_HOST_ASYNC) != 0);
   });

@@ -88,57 +88,82 @@ class PrefetchLoader:
         self._dev = self.device.index
         self._inflight = collections.deque()
         self._n = 0
+        # seed batches read ahead of their submission, each with the event recorded on the
+        # caller's stream when it was read (its batch stream waits on that, not on C's tail)
+        self._pulled = collections.deque()
+        self._events = [torch.cuda.Event() for _ in range(depth + 2)]
+        self._ev_n = 0
 
     def _caller_stream(self):
         if _raw_stream is not None:
             return _raw_stream(self._dev)
         return torch.cuda.current_stream(self.device).cuda_stream
 
-    # Stream ordering.  B waits for C before the launches (the seeds may be produced on C; the
-    # wait is requested by a flag, since C is often the null stream, handle 0), and C waits for
-    # B before the outputs are used.  A batch's sample outputs are allocated from the pool of
-    # the batch stream B that writes them and recorded on C when handed out, so the caching
-    # allocator reuses that memory only after both streams' uses.  (Round 4 root cause of the
-    # round-3 N = 2 corruption: the C-ABI entry point skipped B's wait when C was the null
-    # stream, and rounds 2-3 allocated the outputs on C -- a later batch's buffer could be
-    # carved from an x whose feature gather was still queued on C, and that gather overwrote
+    def _caller_obj(self, cur):
+        if cur != self._c_raw:
+            self._c_raw, self._c_obj = cur, torch.cuda.current_stream(self.device)
+        return self._c_obj
+
+    # Stream ordering.  Each batch stream B waits, before its launches, on an event recorded on
+    # the caller's stream C when the batch's seeds were read from the iterator (they may be
+    # produced on C), and C waits for B before the outputs are used.  Seeds are read one batch
+    # ahead, before the previous batch's gathers go on C, so B does not also wait for those
+    # (round 4: waiting for C's whole tail at submission cost the 3-deep pipeline 7 %).  A
+    # batch's sample outputs are allocated from B's pool and recorded on C when handed out, so
+    # the caching allocator reuses that memory only after both streams' uses.  (Round 4 root
+    # cause of the round-3 N = 2 corruption: the C-ABI entry point skipped B's wait when C was
+    # the null stream, and rounds 2-3 allocated the outputs on C -- a later batch's buffer could
+    # be carved from an x whose feature gather was still queued on C, and that gather overwrote
     # the sampler's output; tests/test_loader_order_gpu.py.)
-    def _submit(self):
+    def _pull(self, cur):
         try:
             seeds = next(self._seeds)
         except StopIteration:
             self._exhausted = True
             return
+        ev = self._events[self._ev_n % len(self._events)]
+        self._ev_n += 1
+        ev.record(self._caller_obj(cur))
+        self._pulled.append((seeds, ev))
+
+    def _submit(self, cur):
+        if not self._pulled:
+            self._pull(cur)
+            if not self._pulled:
+                return
+        seeds, ev = self._pulled.popleft()
         w = self._n % len(self._st)
         st = self._st[w]
         self._n += 1
-        cur = self._caller_stream()
         # the caller may drop its seeds at once: their memory must outlive B's reads
         seeds.record_stream(self._streams[w])
         # int64 seeds (converted on C if need be) + one output buffer from B's pool
         prep = self.sampler._prepare(seeds, self.fan_out, packed=True,
                                      alloc_stream=self._ids[w])
-        if prep[0] is not seeds:
+        # B waits, then the call is enqueued: one C-ABI call.  B is not touched again before
+        # result(): the sampler's launcher thread may issue the launches.  The sampler draws
+        # the launch seeds once it has accepted the call.
+        if prep[0] is not seeds:  # converted on C just now: B waits for C's tail
             prep[0].record_stream(self._streams[w])
-        # B waits for C (after the allocations), then the call is enqueued: one C-ABI call.
-        # B is not touched again before result(): the sampler's launcher thread may issue
-        # the launches.  The sampler draws the launch seeds once it has accepted the call.
-        pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, _HOST_ASYNC,
-                                               st, wait_for=cur)
+            pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, _HOST_ASYNC,
+                                                   st, wait_for=cur)
+        else:
+            pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, _HOST_ASYNC,
+                                                   st, wait_event=ev.cuda_event)
         self._inflight.append((pending, prep[0], w))
 
     def __iter__(self):
         return self
 
     def __next__(self):
-        while not self._exhausted and len(self._inflight) < len(self._st):
-            self._submit()
+        cur = self._caller_stream()
+        while (self._pulled or not self._exhausted) and len(self._inflight) < len(self._st):
+            self._submit(cur)
         if not self._inflight:
             self.close()  # returns the streams
             raise StopIteration
         pending, s64, w = self._inflight.popleft()
         st = self._st[w]
-        cur = self._caller_stream()
         buf = pending.buffer
         try:
             blocks = pending.result(cast=False)
@@ -147,9 +172,10 @@ class PrefetchLoader:
             self.close()
             raise
         if buf is not None:  # the outputs' memory is used on C from here on
-            if cur != self._c_raw:
-                self._c_raw, self._c_obj = cur, torch.cuda.current_stream(self.device)
-            buf.record_stream(self._c_obj)
+            buf.record_stream(self._caller_obj(cur))
+        # the next batch's seeds are read now, before this batch's gathers go on C
+        if not self._pulled and not self._exhausted:
+            self._pull(cur)
         # C after B (the sample call); the feature and label gathers then run on C, whose
         # hardware queue the batch streams do not use -- the wait and both gathers in one
         # C-ABI call.  (The label gather depends on the seeds only; on C it stays off the
@@ -188,6 +214,7 @@ class PrefetchLoader:
                 pass
             dgs.ops._stream_wait(self._st[w], cur)
         self._exhausted = True
+        self._pulled.clear()
         if self._streams:
             _return_streams(self.device, self._streams)
             self._streams, self._st, self._ids = [], [], []

@@ -48,6 +48,7 @@ _SIGS = {
     "dgs_index_select": (c_int, [c_vp, c_i64, c_vp, c_int, c_i64, c_vp, c_vp]),
     "dgs_index_select_device": (c_int, [c_vp, c_i64, c_vp, c_int, c_i64, c_vp, c_vp]),
     "dgs_stream_wait": (c_int, [c_vp, c_vp]),
+    "dgs_stream_wait_event": (c_int, [c_vp, c_vp]),
     "dgs_sample_neighbors": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp,
                                      p_i64, c_vp]),
     "dgs_relabel": (c_int, [p_vp, p_i64, c_int, p_vp, p_i64, c_int, c_vp, p_i64, p_vp, c_vp]),
@@ -65,6 +66,8 @@ _SIGS = {
     "dgs_sampler_bounds": (c_int, [c_vp, c_i64, p_i64, c_int, p_i64, p_i64]),
     "dgs_sampler_sample": (c_int, [c_vp, c_vp, c_i64, p_i64, c_int, c_int, p_vp, p_vp, p_vp,
                                    p_i64, c_vp]),
+    "dgs_sampler_sample_packed": (c_int, [c_vp, c_vp, c_i64, p_i64, c_int, c_int, c_vp, p_i64,
+                                          c_vp]),
     "dgs_sampler_sample_begin": (c_int, [c_vp, c_vp, c_i64, p_i64, c_int, c_int, p_vp, p_vp,
                                          p_vp, ctypes.POINTER(c_u64), c_int, c_vp]),
     "dgs_sampler_sample_end": (c_int, [c_vp, c_int, p_i64, c_vp]),

@@ -123,17 +123,23 @@ class P2PCacheSampler:
                                     stream_ptr(prep[0].device))
 
     def _begin_prepared(self, seeds, prep, replace, launch_seeds, host_async, stream,
-                        wait_for=None):
+                        wait_for=None, wait_event=None):
         """Enqueues a call whose int64 seeds and output buffer _prepare made, on `stream`
-        (a c_void_p or int HIP stream).  PrefetchLoader allocates on the caller's stream and
-        orders the batch stream after those allocations before it launches: `wait_for` (an int
-        HIP stream) makes `stream` wait for it first, in the same C-ABI call."""
+        (a c_void_p or int HIP stream), in one C-ABI call with the batch stream's wait:
+        `wait_for` (an int HIP stream, 0 = the null stream) makes `stream` wait for the work
+        enqueued on it so far; `wait_event` (an int hipEvent_t) makes it wait on that event."""
         s, L, fo, caps, total, buf, ptrs = prep
         st = stream if isinstance(stream, c_vp) else c_vp(stream)
         ls = None
         if L and launch_seeds is not None:
             ls = (ctypes.c_uint64 * L)(*[int(x) & 0xFFFFFFFFFFFFFFFF for x in launch_seeds])
-        if L and wait_for is not None:
+        if L and wait_event is not None:
+            check(lib.dgs_sampler_sample_begin_after(self._h, wait_event, s.data_ptr(),
+                                                     s.numel(), fo, L, int(bool(replace)),
+                                                     buf.data_ptr(), ls,
+                                                     _SAMPLE_WAIT_EVENT | (1 if host_async else 0),
+                                                     st))
+        elif L and wait_for is not None:
             # the wait is requested by the flag: wait_for may be 0, the null stream
             check(lib.dgs_sampler_sample_begin_after(self._h, wait_for, s.data_ptr(),
                                                      s.numel(), fo, L, int(bool(replace)),
@@ -144,6 +150,8 @@ class P2PCacheSampler:
             check(lib.dgs_sampler_sample_begin(self._h, c_vp(s.data_ptr()), s.numel(), fo, L,
                                                int(bool(replace)), *ptrs, ls,
                                                1 if host_async else 0, st))
+        elif wait_event is not None:
+            check(lib.dgs_stream_wait_event(c_vp(wait_event), st))
         elif wait_for is not None:
             check(lib.dgs_stream_wait(c_vp(wait_for), st))
         return _PendingSample(self, seeds, s, L, caps, total, buf, st)
@@ -151,12 +159,13 @@ class P2PCacheSampler:
     def _sample(self, seeds, fan_out, replace, launch_seeds):
         if launch_seeds is not None:
             return self._sample_seeded(seeds, fan_out, replace, launch_seeds)
-        s, L, fo, caps, total, buf, ptrs = self._prepare(seeds, fan_out)
+        s, L, fo, caps, total, buf, _ = self._prepare(seeds, fan_out, packed=True)
         if L == 0:
             return []
         sizes = (c_i64 * (3 * L))()
-        check(lib.dgs_sampler_sample(self._h, c_vp(s.data_ptr()), s.numel(), fo, L,
-                                     int(bool(replace)), *ptrs, sizes, stream_ptr(s.device)))
+        check(lib.dgs_sampler_sample_packed(self._h, s.data_ptr(), s.numel(), fo, L,
+                                            int(bool(replace)), buf.data_ptr(), sizes,
+                                            stream_ptr(s.device)))
         return self._views(seeds, buf, caps, total, sizes, L)
 
     def _prepare(self, seeds, fan_out, packed=False, alloc_stream=None):
@@ -201,19 +210,23 @@ class P2PCacheSampler:
         return s, L, fo, caps, total, buf, None if packed else plan_ptrs(buf.data_ptr(), caps)
 
     def _views(self, seeds, buf, caps, total, sizes, L, cast=True):
-        # per hop [frontier f | rows e | cols e]: the three live prefixes, by slicing (cheaper
-        # on the host than one split into every piece and pad)
-        out = []
-        cur = seeds
-        cast = cast and self._id_dtype != torch.int64
-        off = 0
+        # per hop [frontier f | rows e | cols e]: the three live prefixes and the pads after
+        # them, as ONE split (round 4: one split_with_sizes into 6L pieces costs the host about
+        # 2/3 of 3L separate slices, each of which is a full Python indexing call)
+        parts = []
         for h in range(L):
             f, e = caps[h]
             U, nnz = sizes[3 * h + 1], sizes[3 * h + 2]
-            fr = buf[off:off + U]
-            r = buf[off + f:off + f + nnz]
-            c = buf[off + f + e:off + f + e + nnz]
-            off += f + 2 * e
+            parts += (U, f - U, nnz, e - nnz, nnz, e - nnz)
+        rest = buf.numel() - total
+        if rest:
+            parts.append(rest)
+        pieces = torch.split_with_sizes(buf, parts)
+        out = []
+        cur = seeds
+        cast = cast and self._id_dtype != torch.int64
+        for h in range(L):
+            fr, r, c = pieces[6 * h], pieces[6 * h + 2], pieces[6 * h + 4]
             if cast:
                 fr, r, c = fr.to(self._id_dtype), r.to(self._id_dtype), c.to(self._id_dtype)
             out.append((cur, fr, r, c))
@@ -331,6 +344,7 @@ class P2PCacheFeatureServer:
 
 
 _SAMPLE_WAIT = 2  # DGS_SAMPLE_WAIT (include/dgs_amd.h)
+_SAMPLE_WAIT_EVENT = 4  # DGS_SAMPLE_WAIT_EVENT
 _get_stream = getattr(torch._C, "_cuda_getCurrentStream", None)
 _set_stream = getattr(torch._C, "_cuda_setStream", None)
 

@@ -178,6 +178,13 @@ int dgs_sampler_sample(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
                        const int64_t *fan_out, int L, int replace, int64_t *const *frontiers,
                        int64_t *const *rows, int64_t *const *cols, int64_t *sizes_out,
                        void *stream);
+/* ADDITIVE: dgs_sampler_sample with every hop's outputs packed in one device buffer `out` (per
+ * hop h: frontier[fcap_h], rows[ecap_h], cols[ecap_h] back to back, the capacities of
+ * dgs_sampler_bounds); `seeds` must be device memory.  What the Python binding's
+ * _CAPI_sample_node_classifiction calls: no per-hop pointer arrays to build per call. */
+int dgs_sampler_sample_packed(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
+                              const int64_t *fan_out, int L, int replace, int64_t *out,
+                              int64_t *sizes_out, void *stream);
 /* ADDITIVE: dgs_sampler_sample in two halves.  _begin enqueues every hop on `stream` and
  * returns without waiting; _end waits for that call's sizes (same `stream`, same L).  At most
  * one call per stream is outstanding.  launch_seeds: the L per-hop launch seeds (hop h uses
@@ -189,6 +196,9 @@ int dgs_sampler_sample(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
  * until _end returns.  The output buffers and seeds must stay alive until _end. */
 #define DGS_SAMPLE_HOST_ASYNC 1
 #define DGS_SAMPLE_WAIT 2 /* dgs_sampler_sample_begin_after: wait for `wait_for` first */
+/* dgs_sampler_sample_begin_after: `wait_for` is a hipEvent_t the caller recorded (e.g. where
+ * its seeds were complete); `stream` waits on it first */
+#define DGS_SAMPLE_WAIT_EVENT 4
 int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
                              const int64_t *fan_out, int L, int replace,
                              int64_t *const *frontiers, int64_t *const *rows,
@@ -196,7 +206,8 @@ int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_see
                              void *stream);
 int dgs_sampler_sample_end(dgs_sampler *s, int L, int64_t *sizes_out, void *stream);
 /* ADDITIVE: with DGS_SAMPLE_WAIT in `flags`, `stream` first waits for the work enqueued on
- * `wait_for` so far (any stream, NULL = the null stream); then dgs_sampler_sample_begin with
+ * `wait_for` so far (any stream, NULL = the null stream); with DGS_SAMPLE_WAIT_EVENT it waits on
+ * the event `wait_for`; then dgs_sampler_sample_begin with
  * every hop's outputs packed in one device buffer `out`:
  * per hop h, frontier[fcap_h], rows[ecap_h], cols[ecap_h] back to back (the capacities of
  * dgs_sampler_bounds) -- one call per batch for a pipelined loader.  `seeds` must be device
@@ -240,6 +251,8 @@ int dgs_feature_server_gather(dgs_feature_server *s, const int64_t *nids, int64_
                               void *out, void *stream);
 int dgs_feature_server_local_cache(const dgs_feature_server *s, const void **ptr,
                                    int64_t *rows);
+/* ADDITIVE: `consumer` waits on a hipEvent_t the caller recorded (hipStreamWaitEvent). */
+int dgs_stream_wait_event(void *event, void *consumer);
 /* ADDITIVE (PrefetchLoader, one call per batch): `consumer` waits for `producer` (the batch's
  * sample call), then on `consumer` the feature gather of nids[n] into feat_out (fs may be
  * NULL) and, when labels != NULL, label_out[i] = labels[seeds[i]] (rows of label_row_bytes,
