@@ -1279,14 +1279,6 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
   uint2 kk;
   float T = 0.0f, cx = 0.0f;
   bool skip = false;
-  // Adaptive threshold (round 4): each lane keeps the largest key_lower() of the candidates it
-  // appended in the current row; every kRefresh appends of the half-wave, the k-th largest of
-  // the 32 lane maxima -- the lower bounds of k distinct edges' keys, so at most the row's k-th
-  // key -- replaces T when larger.  Later chunks of the row then pass about k / (edges seen)
-  // instead of k / 4096 (the boot sample): fewer candidates on long rows, same picks.
-  float lmax = -__builtin_inff();
-  int32_t nref = 0;
-  const int32_t kRefresh = a.k < 8 ? 8 : (int32_t)a.k;
   auto load_row = [&](int64_t hh) {
     hstart = (uint32_t)a.hub.cptr[hh];
     hnext = hh + 1 < H ? (uint32_t)a.hub.cptr[hh + 1] : (uint32_t)total;
@@ -1304,8 +1296,6 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
     if (skip && l == 0) a.cand.cnt[hh] = INT32_MAX;
     cb = (uint32_t)a.cand.base[hh];
     cap = a.cand.cap[hh];
-    lmax = -__builtin_inff();
-    nref = 0;
   };
   load_row(h);
   uint32_t carry[4] = {0u, 0u, 0u, 0u};
@@ -1372,12 +1362,10 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
       const int t = has ? __builtin_ctz(m) : 0;
       m &= m - 1;
       uint32_t wt = w2[0], wt1 = w2[1];
-      float pt = p[0];
 #pragma unroll
       for (int e = 1; e < kStreamT; ++e) {
         wt = t == e ? w2[e] : wt;
         wt1 = t == e ? w2[e + 1] : wt1;
-        pt = t == e ? p[e] : pt;
       }
       const float ut = curand_uniform_from(bitsel(m1, wt1, wt));
       const uint32_t b = half_ballot(has);
@@ -1391,16 +1379,6 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
           a.cand.key[(size_t)cb + pos] = ut;
           a.cand.idx[(size_t)cb + pos] = (int32_t)(i0 + 32u * t);
         }
-        lmax = fmaxf(lmax, key_lower(ut, pt));
-      }
-      nref += (int32_t)__builtin_popcount(b);
-    }
-    if (nref >= kRefresh) {  // half-wave uniform
-      nref = 0;
-      const float tk = __shfl(sort32_desc(lmax, l), (int)a.k - 1, 32);
-      if (tk > T) {
-        T = tk;
-        cx = lin_cx(T);
       }
     }
   }
