@@ -169,6 +169,8 @@ constexpr int64_t kBiasSampleSteps = DGS_BIAS_SAMPLE_STEPS;
 #endif
 constexpr int kStreamT = DGS_BIAS_STREAM_T;
 constexpr int kStreamChunk = 32 * kStreamT;
+// Candidates k_bias_stream holds per half-wave in LDS before appending them to the rows' lists.
+constexpr int kStreamBuf = 128;
 
 static_assert(kStreamT % 4 == 0, "whole Philox blocks per chunk");
 // Candidate room of the streamed rows.  The sample threshold lets about k * deg / P of a row's
@@ -1273,11 +1275,10 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
   const uint32_t c1 = (uint32_t)bias_worker_c0(total, wk + 1, nw);
   if (c0 >= c1) return;
   int64_t h = group_search<32>(a.hub.cptr, H, c0);
-  uint32_t hstart = 0, hnext = 0, deg = 0, jb = 0, sub = 0, cb = 0;
-  int32_t cap = 0;
+  uint32_t hstart = 0, hnext = 0, deg = 0, jb = 0, sub = 0;
   global_ptr<float> pr = nullptr;
   uint2 kk;
-  float T = 0.0f, cx = 0.0f;
+  float cx = 0.0f;
   bool skip = false;
   auto load_row = [&](int64_t hh) {
     hstart = (uint32_t)a.hub.cptr[hh];
@@ -1288,18 +1289,67 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
     sub = c.sub;
     kk = c.kk;
     pr = c.pr;
-    T = key_from_order((int32_t)a.hub.thr[hh]);
+    const float T = key_from_order((int32_t)a.hub.thr[hh]);
     cx = lin_cx(T);
     // no finite sample threshold (weights <= 0): every edge would be a candidate; the merge
     // recomputes the row instead (every worker of the row stores the same marker)
     skip = !(T > -__builtin_inff());
     if (skip && l == 0) a.cand.cnt[hh] = INT32_MAX;
-    cb = (uint32_t)a.cand.base[hh];
-    cap = a.cand.cap[hh];
+  };
+  // Chunk q's probabilities (the last edge's repeated past the row's end).
+  auto load_probs = [&](uint32_t q, float *p) {
+    const uint32_t i0 = q * kStreamChunk + l;
+    const bool whole = q * kStreamChunk + kStreamChunk <= deg;
+#pragma unroll
+    for (int t = 0; t < kStreamT; ++t) {
+      const uint32_t i = i0 + 32u * t;
+      p[t] = pr[whole ? i : (i < deg - 1u ? i : deg - 1u)];
+    }
+  };
+  // Candidates wait in this half-wave's LDS list as (draw, edge, hub row) and reach their rows'
+  // global lists in batches (one returning atomic per row and batch).  An atomic per chunk made
+  // every chunk wait out a memory round trip, and that wait also drained the next chunk's
+  // probability loads.
+  __shared__ uint32_t s_x[kTileRows / 32][kStreamBuf], s_i[kTileRows / 32][kStreamBuf];
+  __shared__ int32_t s_h[kTileRows / 32][kStreamBuf];
+  const int g = threadIdx.x >> 5;
+  int nb = 0;  // entries in the list (half-wave uniform)
+  auto flush = [&]() {
+    __builtin_amdgcn_wave_barrier();
+    for (int e0 = 0; e0 < nb; e0 += 32) {
+      const int e = e0 + l;
+      const bool v = e < nb;
+      const uint32_t x = v ? s_x[g][e] : 0u;
+      const uint32_t ix = v ? s_i[g][e] : 0u;
+      const int32_t hh = v ? s_h[g][e] : -1;
+      uint32_t todo = half_ballot(v);
+      while (todo) {
+        const int lead = __builtin_ctz(todo);
+        const int32_t hl = __shfl(hh, lead, 32);
+        const uint32_t same = half_ballot(v & (hh == hl));
+        int32_t old = 0;
+        if (l == lead) old = atomicAdd(a.cand.cnt + hl, (int32_t)__builtin_popcount(same));
+        old = __shfl(old, lead, 32);
+        if ((same >> l) & 1u) {
+          const int32_t pos = old + (int32_t)__builtin_popcount(same & ((1u << l) - 1u));
+          if (pos < a.cand.cap[hl]) {
+            const size_t o = (size_t)a.cand.base[hl] + (size_t)pos;
+            a.cand.key[o] = curand_uniform_from(x);
+            a.cand.idx[o] = (int32_t)ix;
+          }
+        }
+        todo &= ~same;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    nb = 0;
   };
   load_row(h);
   uint32_t carry[4] = {0u, 0u, 0u, 0u};
   uint32_t carry_cb = ~0u;
+  // the next chunk's probabilities, loaded under this chunk's Philox (same row only)
+  float pn[kStreamT];
+  bool have_next = false;
   for (uint32_t ch = c0; ch < c1; ++ch) {
     while (ch >= hnext) {
       ++h;
@@ -1310,12 +1360,12 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
     const uint32_t q = ch - hstart;
     const uint32_t i0 = q * kStreamChunk + l;
     const bool whole = q * kStreamChunk + kStreamChunk <= deg;
+    if (!have_next) load_probs(q, pn);
     float p[kStreamT];
 #pragma unroll
-    for (int t = 0; t < kStreamT; ++t) {
-      const uint32_t i = i0 + 32u * t;
-      p[t] = pr[whole ? i : (i < deg - 1u ? i : deg - 1u)];
-    }
+    for (int t = 0; t < kStreamT; ++t) p[t] = pn[t];
+    have_next = ch + 1 < c1 && ch + 1 < hnext;
+    if (have_next) load_probs(q + 1, pn);
     const uint32_t j0 = jb + q * kStreamT;
     const uint32_t bc = j0 >> 2;
     const int off = (int)(j0 & 3);
@@ -1355,9 +1405,10 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
       m |= (uint32_t)(valid & !lin_reject(bitsel(m1, w2[t + 1], w2[t]), p[t], cx)) << t;
     }
 
-    // the few that pass the bound go to the row's list as (u, edge); the merge computes their
+    // the few that pass the bound go to the list as (draw, edge); the merge computes their
     // exact keys (keeping the fixed-operation key out of this loop saves registers)
     while (half_ballot(m != 0)) {
+      if (nb > kStreamBuf - 32) flush();
       const bool has = m != 0;
       const int t = has ? __builtin_ctz(m) : 0;
       m &= m - 1;
@@ -1367,21 +1418,17 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
         wt = t == e ? w2[e] : wt;
         wt1 = t == e ? w2[e + 1] : wt1;
       }
-      const float ut = curand_uniform_from(bitsel(m1, wt1, wt));
       const uint32_t b = half_ballot(has);
-      const int lead = __builtin_ctz(b);
-      int32_t old = 0;
-      if (l == lead) old = atomicAdd(a.cand.cnt + h, (int32_t)__builtin_popcount(b));
-      old = __shfl(old, lead, 32);
       if (has) {
-        const int32_t pos = old + (int32_t)__builtin_popcount(b & ((1u << l) - 1u));
-        if (pos < cap) {
-          a.cand.key[(size_t)cb + pos] = ut;
-          a.cand.idx[(size_t)cb + pos] = (int32_t)(i0 + 32u * t);
-        }
+        const int pos = nb + __builtin_popcount(b & ((1u << l) - 1u));
+        s_x[g][pos] = bitsel(m1, wt1, wt);
+        s_i[g][pos] = i0 + 32u * t;
+        s_h[g][pos] = (int32_t)h;
       }
+      nb += __builtin_popcount(b);
     }
   }
+  if (nb > 0) flush();
 }
 
 // Candidate e of a streamed row: its exact key from (u, edge) and the row's probabilities.
