@@ -1723,15 +1723,20 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
           DGS_HIP(hipMemcpy(cnt.data(), cand.cnt, 4 * H, hipMemcpyDeviceToHost));
           DGS_HIP(hipMemcpy(cap.data(), cand.cap, 4 * H, hipMemcpyDeviceToHost));
         }
-        int64_t tot = 0, over = 0, mx = 0, big64 = 0;
+        int64_t tot = 0, over = 0, mx = 0, big64 = 0, big256 = 0, in256 = 0;
         for (int64_t h = 0; h < H; ++h) {
           if (cnt[(size_t)h] > cap[(size_t)h]) { ++over; continue; }
           tot += cnt[(size_t)h];
           mx = std::max<int64_t>(mx, cnt[(size_t)h]);
           big64 += cnt[(size_t)h] > 64;
+          big256 += cnt[(size_t)h] > 256;
+          in256 += cnt[(size_t)h] > 256 ? cnt[(size_t)h] : 0;
         }
-        fprintf(stderr, "[bias stats] candidates %lld (max %lld, rows > 64: %lld) overflowed rows %lld\n",
-                (long long)tot, (long long)mx, (long long)big64, (long long)over);
+        fprintf(stderr,
+                "[bias stats] candidates %lld (max %lld, rows > 64: %lld, rows > 256: %lld holding "
+                "%lld) overflowed rows %lld\n",
+                (long long)tot, (long long)mx, (long long)big64, (long long)big256,
+                (long long)in256, (long long)over);
       }
     }
     if (replace) {
