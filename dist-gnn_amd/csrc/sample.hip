@@ -169,8 +169,9 @@ constexpr int64_t kBiasSampleSteps = DGS_BIAS_SAMPLE_STEPS;
 #endif
 constexpr int kStreamT = DGS_BIAS_STREAM_T;
 constexpr int kStreamChunk = 32 * kStreamT;
-// Candidates k_bias_stream holds per half-wave in LDS before appending them to the rows' lists.
-constexpr int kStreamBuf = 128;
+// Candidates k_bias_stream holds per half-wave in LDS before appending them to the rows' lists
+// (a flush when more than 64 wait; a chunk adds at most kStreamChunk).
+constexpr int kStreamBuf = 64 + kStreamChunk;
 
 static_assert(kStreamT % 4 == 0, "whole Philox blocks per chunk");
 // Candidate room of the streamed rows.  The sample threshold lets about k * deg / P of a row's
@@ -1141,8 +1142,18 @@ __device__ __forceinline__ void tree_merge8(const HalfTopK &top, int64_t k, int 
 __device__ __forceinline__ float lin_cx(float T) {
   return T * (0.6931471805599453f * 1.0000152587890625f) * 4294967296.0f;
 }
-__device__ __forceinline__ bool lin_reject(uint32_t x, float p, float cx) {
-  return (float)x < __builtin_fmaf(p, cx, 4294962688.0f);
+// The test as the kernel uses it: the lanes of the wave where it does NOT reject, i.e.
+// !((float)x < p cx + bx) -- >= or unordered -- as the compare's own 64-bit result (active
+// lanes only; a ballot of the predicate would first materialise it in a VGPR).
+__device__ __forceinline__ uint64_t lin_pass_mask(uint32_t x, float p, float cx) {
+  return __builtin_amdgcn_fcmpf((float)x, __builtin_fmaf(p, cx, 4294962688.0f), 11 /*UGE*/);
+}
+// (mask & a) | (~mask & b) in one v_bfi_b32 (a ternary on an all-ones / zero mask became a
+// compare and a select)
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "v"(a), "v"(b));
+  return r;
 }
 
 // A value <= ares_key(u, p) for every u in (0, 1] and p: the hardware log2 (v_log_f32, within a
@@ -1297,13 +1308,19 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
     if (skip && l == 0) a.cand.cnt[hh] = INT32_MAX;
   };
   // Chunk q's probabilities (the last edge's repeated past the row's end).
+  // (a whole chunk: one address and immediate offsets; the kernel is VALU-issue-bound)
   auto load_probs = [&](uint32_t q, float *p) {
     const uint32_t i0 = q * kStreamChunk + l;
-    const bool whole = q * kStreamChunk + kStreamChunk <= deg;
+    if (q * kStreamChunk + kStreamChunk <= deg) {
+      const global_ptr<float> pc = pr + i0;
 #pragma unroll
-    for (int t = 0; t < kStreamT; ++t) {
-      const uint32_t i = i0 + 32u * t;
-      p[t] = pr[whole ? i : (i < deg - 1u ? i : deg - 1u)];
+      for (int t = 0; t < kStreamT; ++t) p[t] = pc[32 * t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < kStreamT; ++t) {
+        const uint32_t i = i0 + 32u * t;
+        p[t] = pr[i < deg - 1u ? i : deg - 1u];
+      }
     }
   };
   // Candidates wait in this half-wave's LDS list as (draw, edge, hub row) and reach their rows'
@@ -1395,33 +1412,30 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
     const uint32_t m2 = (off & 2) ? ~0u : 0u, m1 = (off & 1) ? ~0u : 0u;
     uint32_t w2[kStreamT + 1];
 #pragma unroll
-    for (int e = 0; e < kStreamT + 1; ++e) w2[e] = bitsel(m2, wv[e + 2], wv[e]);
-    uint32_t m = 0;  // bit t: edge i0 + 32 t passed the cheap bound
-    // Reject when key < T is certain (lin_reject: one convert, one fma and one compare per
-    // edge; round 3 A/B against the hardware-log2 bound: stream kernel 35.1 -> 33.5 us, +1.7 %).
+    for (int e = 0; e < kStreamT + 1; ++e) w2[e] = bfi(m2, wv[e + 2], wv[e]);
+    // Per step t, the wave's lanes whose edge passes the cheap bound, straight from the compares
+    // (lin_pass_mask: one convert, one fma and one compare per edge; round 3 A/B against the
+    // hardware-log2 bound: +1.7 %); the valid-edge compare only matters in a row's last chunk.
+    const uint64_t whole_mask = __ballot(whole);
+    uint32_t xs[kStreamT];
+    uint64_t pass[kStreamT];
 #pragma unroll
     for (int t = 0; t < kStreamT; ++t) {
-      const bool valid = whole | (i0 + 32u * t < deg);
-      m |= (uint32_t)(valid & !lin_reject(bitsel(m1, w2[t + 1], w2[t]), p[t], cx)) << t;
+      xs[t] = bfi(m1, w2[t + 1], w2[t]);
+      const uint64_t valid = whole_mask | __builtin_amdgcn_uicmp(i0 + 32u * t, deg, 36 /*ULT*/);
+      pass[t] = valid & lin_pass_mask(xs[t], p[t], cx);
     }
-
-    // the few that pass the bound go to the list as (draw, edge); the merge computes their
-    // exact keys (keeping the fixed-operation key out of this loop saves registers)
-    while (half_ballot(m != 0)) {
-      if (nb > kStreamBuf - 32) flush();
-      const bool has = m != 0;
-      const int t = has ? __builtin_ctz(m) : 0;
-      m &= m - 1;
-      uint32_t wt = w2[0], wt1 = w2[1];
+    // the few that pass go to the list as (draw, edge); the merge computes their exact keys
+    // (keeping the fixed-operation key out of this loop saves registers)
+    if (nb > kStreamBuf - kStreamChunk) flush();
+    const int hs = threadIdx.x & 32;
 #pragma unroll
-      for (int e = 1; e < kStreamT; ++e) {
-        wt = t == e ? w2[e] : wt;
-        wt1 = t == e ? w2[e + 1] : wt1;
-      }
-      const uint32_t b = half_ballot(has);
-      if (has) {
+    for (int t = 0; t < kStreamT; ++t) {
+      if (pass[t] == 0) continue;
+      const uint32_t b = (uint32_t)(pass[t] >> hs);
+      if ((b >> l) & 1u) {
         const int pos = nb + __builtin_popcount(b & ((1u << l) - 1u));
-        s_x[g][pos] = bitsel(m1, wt1, wt);
+        s_x[g][pos] = xs[t];
         s_i[g][pos] = i0 + 32u * t;
         s_h[g][pos] = (int32_t)h;
       }
@@ -1542,8 +1556,9 @@ __global__ __launch_bounds__(kTileRows) void k_bias_hub_merge(BiasHubArgs a) {
 }
 
 // Test-only (dgs_test_bias_bounds): the exact A-Res key, key_lower() and the two reject tests
-// the biased kernels use (bit 0: the stream kernel's lin_reject against T; bit 1: the row /
-// hub-run filter !ares_may_pass_s against thr = T), per (draw x, probability p, threshold T).
+// the biased kernels use (bit 0: the stream kernel's linear reject against T, read from the wave
+// mask it uses; bit 1: the row / hub-run filter !ares_may_pass_s against thr = T), per (draw x,
+// probability p, threshold T).
 __global__ void k_test_bias_bounds(const uint32_t *x, const float *p, const float *thr, int64_t n,
                                    float *key, float *klow, uint8_t *flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1552,8 +1567,9 @@ __global__ void k_test_bias_bounds(const uint32_t *x, const float *p, const floa
   const float pi = p[i], T = thr[i];
   key[i] = ares_key(u, pi);
   klow[i] = key_lower(u, pi);
-  flags[i] = (uint8_t)((int)lin_reject(x[i], pi, lin_cx(T)) |
-                       ((int)!ares_may_pass_s(u, pi, slack_thr(T)) << 1));
+  // the stream kernel's form: the lane's bit of the wave's pass mask
+  const bool pass = (lin_pass_mask(x[i], pi, lin_cx(T)) >> (threadIdx.x & 63)) & 1u;
+  flags[i] = (uint8_t)((int)!pass | ((int)!ares_may_pass_s(u, pi, slack_thr(T)) << 1));
 }
 
 }  // namespace
