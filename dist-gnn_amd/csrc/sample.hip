@@ -1416,14 +1416,18 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
     // Per step t, the wave's lanes whose edge passes the cheap bound, straight from the compares
     // (lin_pass_mask: one convert, one fma and one compare per edge; round 3 A/B against the
     // hardware-log2 bound: +1.7 %); the valid-edge compare only matters in a row's last chunk.
-    const uint64_t whole_mask = __ballot(whole);
     uint32_t xs[kStreamT];
     uint64_t pass[kStreamT];
 #pragma unroll
     for (int t = 0; t < kStreamT; ++t) {
       xs[t] = bfi(m1, w2[t + 1], w2[t]);
-      const uint64_t valid = whole_mask | __builtin_amdgcn_uicmp(i0 + 32u * t, deg, 36 /*ULT*/);
-      pass[t] = valid & lin_pass_mask(xs[t], p[t], cx);
+      pass[t] = lin_pass_mask(xs[t], p[t], cx);
+    }
+    const uint64_t whole_mask = __ballot(whole);
+    if (whole_mask != __builtin_amdgcn_read_exec()) {  // (wave-uniform: a row's last chunk)
+#pragma unroll
+      for (int t = 0; t < kStreamT; ++t)
+        pass[t] &= whole_mask | __builtin_amdgcn_uicmp(i0 + 32u * t, deg, 36 /*ULT*/);
     }
     // the few that pass go to the list as (draw, edge); the merge computes their exact keys
     // (keeping the fixed-operation key out of this loop saves registers)
