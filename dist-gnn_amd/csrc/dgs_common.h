@@ -173,6 +173,35 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
   return c;
 }
 
+// The ten round keys of philox4x32_10 (for a loop over many blocks under one key: the schedule's
+// additions once, not per block).
+struct PhiloxKeys {
+  uint32_t x[10], y[10];
+};
+__device__ __forceinline__ PhiloxKeys philox_keys(uint2 k) {
+  PhiloxKeys K;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    K.x[r] = k.x + (uint32_t)r * 0x9E3779B9u;
+    K.y[r] = k.y + (uint32_t)r * 0xBB67AE85u;
+  }
+  return K;
+}
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, const PhiloxKeys &K) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    if (r == 0)
+      c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ K.x[0], (uint32_t)p1,
+                     (uint32_t)(p0 >> 32) ^ c.w ^ K.y[0], (uint32_t)p0);
+    else
+      c = make_uint4(xor3((uint32_t)(p1 >> 32), c.y, K.x[r]), (uint32_t)p1,
+                     xor3((uint32_t)(p0 >> 32), c.w, K.y[r]), (uint32_t)p0);
+  }
+  return c;
+}
+
 // Issue priority of the latency-bound per-hop kernels (prep, row sampling, compaction,
 // relabel) over co-resident waves of the throughput-bound hub kernels of other batches in
 // flight (s_setprio; 0 = the hardware default).

@@ -174,6 +174,11 @@ constexpr int kStreamChunk = 32 * kStreamT;
 constexpr int kStreamBuf = 64 + kStreamChunk;
 
 static_assert(kStreamT % 4 == 0, "whole Philox blocks per chunk");
+// Chunks of a streamed row: its lanes' steps shifted by up to 3 (k_bias_stream aligns a lane's
+// chunks to its Philox blocks), at most deg / kStreamChunk + 2.
+__host__ __device__ __forceinline__ int64_t bias_stream_chunks(int64_t deg) {
+  return ((deg + 31) / 32 + 3 + kStreamT - 1) / kStreamT;
+}
 // Candidate room of the streamed rows.  The sample threshold lets about k * deg / P of a row's
 // edges through (P = min(deg, 4096) sampled edges), i.e. about k for rows the sample covers and
 // k / 32 per 128-edge chunk for larger ones.  The room is linear in the row's chunk range, so it
@@ -250,7 +255,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
       const bool is_hub = a.use_hubs == 1 ? deg - k > kHubT : deg > kBiasHubT;
       if (is_hub) {
         const uint64_t nch = a.use_hubs == 1 ? (uint64_t)(deg - k + 511) / 512
-                                             : (uint64_t)(deg + kStreamChunk - 1) / kStreamChunk;
+                                             : (uint64_t)bias_stream_chunks(deg);
         const uint64_t old = atomicAdd((unsigned long long *)a.hub.count,
                                        (unsigned long long)((uint64_t(1) << kHubShift) | nch));
         h = (int64_t)(old >> kHubShift);
@@ -1286,9 +1291,9 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
   const uint32_t c1 = (uint32_t)bias_worker_c0(total, wk + 1, nw);
   if (c0 >= c1) return;
   int64_t h = group_search<32>(a.hub.cptr, H, c0);
-  uint32_t hstart = 0, hnext = 0, deg = 0, jb = 0, sub = 0;
+  uint32_t hstart = 0, hnext = 0, deg = 0, jb = 0, off = 0, sub = 0;
   global_ptr<float> pr = nullptr;
-  uint2 kk;
+  PhiloxKeys kk;
   float cx = 0.0f;
   bool skip = false;
   auto load_row = [&](int64_t hh) {
@@ -1297,8 +1302,9 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
     const HubRowCtx c = hub_row_ctx(a, hh, G, l);
     deg = (uint32_t)c.deg;
     jb = (uint32_t)c.jb;
+    off = jb & 3u;
     sub = c.sub;
-    kk = c.kk;
+    kk = philox_keys(c.kk);
     pr = c.pr;
     const float T = key_from_order((int32_t)a.hub.thr[hh]);
     cx = lin_cx(T);
@@ -1307,19 +1313,30 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
     skip = !(T > -__builtin_inff());
     if (skip && l == 0) a.cand.cnt[hh] = INT32_MAX;
   };
-  // Chunk q's probabilities (the last edge's repeated past the row's end).
-  // (a whole chunk: one address and immediate offsets; the kernel is VALU-issue-bound)
+  // Chunks are aligned to the lane's Philox blocks: lane l's chunk q holds its steps
+  // s = kStreamT q - off + t (t < kStreamT, off = jb mod 4), i.e. draws jb - off + kStreamT q + t,
+  // exactly the words of blocks (jb >> 2) + q kStreamT / 4 + {0, 1}: no draw window to select
+  // from and no block carried between chunks (a row has up to one chunk more for it).  Step s
+  // is edge 32 s + l, valid when 0 <= s and 32 s + l < deg.
+  // The first edge of chunk q in this lane (negative before the row's start) and whether all of
+  // the chunk's edges are valid.
+  auto chunk_i0 = [&](uint32_t q) { return (int32_t)(32u * (q * kStreamT - off) + (uint32_t)l); };
+  auto chunk_whole = [&](int32_t i0) {
+    return i0 >= 0 && (uint32_t)i0 + 32u * (kStreamT - 1) < deg;
+  };
+  // Chunk q's probabilities (clamped into the row outside it; whole chunks: one address and
+  // immediate offsets -- the kernel is VALU-issue-bound).
   auto load_probs = [&](uint32_t q, float *p) {
-    const uint32_t i0 = q * kStreamChunk + l;
-    if (q * kStreamChunk + kStreamChunk <= deg) {
+    const int32_t i0 = chunk_i0(q);
+    if (chunk_whole(i0)) {
       const global_ptr<float> pc = pr + i0;
 #pragma unroll
       for (int t = 0; t < kStreamT; ++t) p[t] = pc[32 * t];
     } else {
 #pragma unroll
       for (int t = 0; t < kStreamT; ++t) {
-        const uint32_t i = i0 + 32u * t;
-        p[t] = pr[i < deg - 1u ? i : deg - 1u];
+        const int32_t i = i0 + 32 * t;
+        p[t] = pr[i < 0 ? 0 : ((uint32_t)i < deg - 1u ? (uint32_t)i : deg - 1u)];
       }
     }
   };
@@ -1362,8 +1379,6 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
     nb = 0;
   };
   load_row(h);
-  uint32_t carry[4] = {0u, 0u, 0u, 0u};
-  uint32_t carry_cb = ~0u;
   // the next chunk's probabilities, loaded under this chunk's Philox (same row only)
   float pn[kStreamT];
   bool have_next = false;
@@ -1371,63 +1386,39 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
     while (ch >= hnext) {
       ++h;
       load_row(h);
-      carry_cb = ~0u;
     }
     if (skip) continue;
     const uint32_t q = ch - hstart;
-    const uint32_t i0 = q * kStreamChunk + l;
-    const bool whole = q * kStreamChunk + kStreamChunk <= deg;
+    const int32_t i0 = chunk_i0(q);
+    const bool whole = chunk_whole(i0);
     if (!have_next) load_probs(q, pn);
     float p[kStreamT];
 #pragma unroll
     for (int t = 0; t < kStreamT; ++t) p[t] = pn[t];
     have_next = ch + 1 < c1 && ch + 1 < hnext;
     if (have_next) load_probs(q + 1, pn);
-    const uint32_t j0 = jb + q * kStreamT;
-    const uint32_t bc = j0 >> 2;
-    const int off = (int)(j0 & 3);
-    uint32_t wv[kStreamT + 4];
-    if (bc == carry_cb) {
+    const uint32_t bc = (jb >> 2) + q * (kStreamT / 4);
+    uint32_t xs[kStreamT];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) wv[e] = carry[e];
-    } else {
-      const uint4 o = philox4x32_10(make_uint4(bc, 0u, sub, 0u), kk);
-      wv[0] = o.x;
-      wv[1] = o.y;
-      wv[2] = o.z;
-      wv[3] = o.w;
-    }
-#pragma unroll
-    for (int bq = 1; bq <= kStreamT / 4; ++bq) {
+    for (int bq = 0; bq < kStreamT / 4; ++bq) {
       const uint4 o = philox4x32_10(make_uint4(bc + bq, 0u, sub, 0u), kk);
-      wv[4 * bq + 0] = o.x;
-      wv[4 * bq + 1] = o.y;
-      wv[4 * bq + 2] = o.z;
-      wv[4 * bq + 3] = o.w;
+      xs[4 * bq + 0] = o.x;
+      xs[4 * bq + 1] = o.y;
+      xs[4 * bq + 2] = o.z;
+      xs[4 * bq + 3] = o.w;
     }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) carry[e] = wv[kStreamT + e];
-    carry_cb = bc + kStreamT / 4;
-    // draw t = word off + t of the window, picked with bit-select masks on the offset
-    const uint32_t m2 = (off & 2) ? ~0u : 0u, m1 = (off & 1) ? ~0u : 0u;
-    uint32_t w2[kStreamT + 1];
-#pragma unroll
-    for (int e = 0; e < kStreamT + 1; ++e) w2[e] = bfi(m2, wv[e + 2], wv[e]);
     // Per step t, the wave's lanes whose edge passes the cheap bound, straight from the compares
     // (lin_pass_mask: one convert, one fma and one compare per edge; round 3 A/B against the
-    // hardware-log2 bound: +1.7 %); the valid-edge compare only matters in a row's last chunk.
-    uint32_t xs[kStreamT];
+    // hardware-log2 bound: +1.7 %); the valid-edge compare only matters in a row's first and
+    // last chunks.
     uint64_t pass[kStreamT];
 #pragma unroll
-    for (int t = 0; t < kStreamT; ++t) {
-      xs[t] = bfi(m1, w2[t + 1], w2[t]);
-      pass[t] = lin_pass_mask(xs[t], p[t], cx);
-    }
+    for (int t = 0; t < kStreamT; ++t) pass[t] = lin_pass_mask(xs[t], p[t], cx);
     const uint64_t whole_mask = __ballot(whole);
-    if (whole_mask != __builtin_amdgcn_read_exec()) {  // (wave-uniform: a row's last chunk)
+    if (whole_mask != __builtin_amdgcn_read_exec()) {  // (wave-uniform: a row's first / last chunk)
 #pragma unroll
-      for (int t = 0; t < kStreamT; ++t)
-        pass[t] &= whole_mask | __builtin_amdgcn_uicmp(i0 + 32u * t, deg, 36 /*ULT*/);
+      for (int t = 0; t < kStreamT; ++t)  // (a negative edge compares as a huge unsigned one)
+        pass[t] &= whole_mask | __builtin_amdgcn_uicmp((uint32_t)(i0 + 32 * t), deg, 36 /*ULT*/);
     }
     // the few that pass go to the list as (draw, edge); the merge computes their exact keys
     // (keeping the fixed-operation key out of this loop saves registers)
@@ -1440,7 +1431,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
       if ((b >> l) & 1u) {
         const int pos = nb + __builtin_popcount(b & ((1u << l) - 1u));
         s_x[g][pos] = xs[t];
-        s_i[g][pos] = i0 + 32u * t;
+        s_i[g][pos] = (uint32_t)(i0 + 32 * t);
         s_h[g][pos] = (int32_t)h;
       }
       nb += __builtin_popcount(b);
@@ -1629,13 +1620,13 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   BiasCand cand{};
   if (bias_hubs) {
     // Hub rows have degree > kBiasHubT and are distinct within a hop: at most
-    // min(S, E / kBiasHubT) of them, with at most E / kStreamChunk + S chunks.  The room is
+    // min(S, E / kBiasHubT) of them, with at most E / kStreamChunk + 2 per hub chunks.  The room is
     // capped by a budget (DGS_BIAS_CAND_BUDGET entries, default 2^26 = 512 MB per context):
     // rows past it get no room and are recomputed exactly (rare; correct either way).
     const int64_t hubs_ub =
         src.num_edges > 0 ? std::min<int64_t>(S, src.num_edges / kBiasHubT + 1) : S;
     const int64_t chunks =
-        src.num_edges > 0 ? src.num_edges / kStreamChunk + hubs_ub : (int64_t(1) << 22);
+        src.num_edges > 0 ? src.num_edges / kStreamChunk + 2 * hubs_ub : (int64_t(1) << 22);
     static const int64_t budget = [] {
       const char *e = getenv("DGS_BIAS_CAND_BUDGET");
       const long long v = e ? atoll(e) : 0;
