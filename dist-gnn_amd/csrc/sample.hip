@@ -1009,8 +1009,8 @@ __device__ __forceinline__ void merge_emit(const BiasHubArgs &a, int64_t S, int6
 //   k_bias_stream  every edge of the row: Philox and a cheap linear bound against T; the few
 //                  that pass go to the row's candidate list as (u, edge).  The bound is
 //                  conservative, so every final pick is kept (they all have key >= final k-th
-//                  >= T).  Half-wave workers over contiguous 128-edge chunk ranges, Philox blocks
-//                  carried across a worker's chunks, no LDS, no exact key (registers).
+//                  >= T).  Half-wave workers over contiguous chunk ranges (each lane's chunks
+//                  aligned to its Philox blocks), candidates staged in LDS, no exact key.
 //   merge          (in k_bias_rows_merge) exact keys of each row's candidates and their top-k;
 //                  a row whose list overflowed (or whose sample had no finite k-th key) is
 //                  recomputed exactly.
