@@ -1173,38 +1173,50 @@ __device__ __forceinline__ float key_lower(float u, float p) {
   return ((p >= 7.888609052210118e-31f) & (p <= 1.2676506002282294e+30f)) ? q : -__builtin_inff();
 }
 
-// Largest key_lower() of this lane's edges in steps [s0, s1) of a row (the Philox window of
-// bias_run; no cross-lane work).  Any value of it is a real edge's lower bound, so the k-th
-// largest over lanes is at most the k-th largest exact key of the sampled edges.
-__device__ __forceinline__ float lane_max_run(const HubRowCtx &c, int64_t s0, int64_t s1, int l) {
+// Largest key_lower() of this lane's edges among its draws [A, E), A = the first block boundary
+// at or after draw jb + s0 and E = min(A + len, the first block boundary at or after jb + s1):
+// whole Philox blocks only (no draw window to select from), and consecutive runs of a row stay
+// disjoint, so the lane maxima of different runs are different edges.  Draw jb + s is step s,
+// edge 32 s + l (valid below deg).  No cross-lane work.
+__device__ __forceinline__ float lane_max_run(const HubRowCtx &c, int64_t s0, int64_t s1,
+                                              int64_t len, int l) {
   float best = -__builtin_inff();
-  const int64_t n = s1 - s0;
-  if (n <= 0) return best;
-  const int64_t j = c.jb + s0;
-  const int64_t bl = j >> 2;
-  const int off = (int)(j & 3);
-  const uint32_t m2 = (off & 2) ? ~0u : 0u, m1 = (off & 1) ? ~0u : 0u;
-  uint4 A = philox4x32_10(make_uint4((uint32_t)bl, (uint32_t)((uint64_t)bl >> 32), c.sub, 0u),
-                          c.kk);
-  const int64_t e0 = 32 * s0 + l;
-  const int64_t e1 = 32 * s1 < c.deg ? 32 * s1 : c.deg;
-  for (int64_t g = 0; 4 * g < n; ++g) {
+  const int64_t A = (c.jb + s0 + 3) & ~int64_t(3);
+  const int64_t E1 = (c.jb + s1 + 3) & ~int64_t(3);
+  const int64_t E = A + len < E1 ? A + len : E1;
+  if (E <= A) return best;
+  const PhiloxKeys K = philox_keys(c.kk);
+  const int32_t nbk = (int32_t)((E - A) >> 2);
+  const uint32_t deg = (uint32_t)c.deg;
+  const uint32_t ib = (uint32_t)(32 * (A - c.jb) + l);  // edge of the run's first draw
+  // block q's probabilities, 0 past the row's end (key_lower(u, 0) = -inf: no select needed);
+  // a block inside the row loads from one address with immediate offsets
+  auto load4 = [&](int32_t q, float *p) {
+    const uint32_t i0 = ib + 128u * (uint32_t)q;
+    if (i0 + 96u < deg) {
+      const global_ptr<float> pc = c.pr + i0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) p[w] = pc[32 * w];
+    } else {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) p[w] = i0 + 32u * w < deg ? c.pr[i0 + 32u * w] : 0.0f;
+    }
+  };
+  // the next block's probabilities load under this block's Philox and keys
+  float pn[4];
+  load4(0, pn);
+  for (int32_t q = 0; q < nbk; ++q) {
     float p[4];
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      const int64_t i = e0 + 128 * g + 32 * s4;
-      p[s4] = i < e1 ? c.pr[i] : 0.0f;
-    }
-    const uint64_t qb = (uint64_t)(bl + g + 1);
-    const uint4 B = philox4x32_10(make_uint4((uint32_t)qb, (uint32_t)(qb >> 32), c.sub, 0u), c.kk);
-    const uint32_t wv[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+    for (int w = 0; w < 4; ++w) p[w] = pn[w];
+    load4(q + 1, pn);
+    const uint64_t qb = (uint64_t)((A >> 2) + q);
+    const uint4 B = philox4x32_10(make_uint4((uint32_t)qb, (uint32_t)(qb >> 32), c.sub, 0u), K);
+    const uint32_t wv[4] = {B.x, B.y, B.z, B.w};
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      const uint32_t w0 = bitsel(m2, wv[s4 + 2], wv[s4]), w1 = bitsel(m2, wv[s4 + 3], wv[s4 + 1]);
-      const float kl = key_lower(curand_uniform_from(bitsel(m1, w1, w0)), p[s4]);
-      best = e0 + 128 * g + 32 * s4 < e1 ? fmaxf(best, kl) : best;
-    }
-    A = B;
+    for (int w = 0; w < 4; ++w)  // (max of two non-NaN values in one v_med3_f32)
+      best = __builtin_amdgcn_fmed3f(key_lower(curand_uniform_from(wv[w]), p[w]), best,
+                                     __builtin_inff());
   }
   return best;
 }
@@ -1225,9 +1237,10 @@ __device__ __forceinline__ float sort32_desc(float v, int l) {
 }
 
 // One workgroup per hub row (grid-stride over the hub list): the row's threshold T.  Half-wave g
-// samples kBiasSampleSteps steps from step ns * g / 8 (the whole row when it has fewer than
-// 8 kBiasSampleSteps steps); the 8 sorted lists of lane maxima are merged pairwise in LDS and
-// the k-th largest of the 256 is T.
+// samples up to kBiasSampleSteps draws from step ns * g / 8 on, cut at block boundaries (its
+// part of the row when the row has fewer than 8 kBiasSampleSteps steps); the 8 sorted lists of
+// lane maxima are merged pairwise in LDS and the k-th largest of the 256 is T (a lower bound of
+// k distinct edges' keys: the runs are disjoint).
 __global__ __launch_bounds__(kTileRows) void k_bias_boot(BiasHubArgs a) {
   latency_prio();
   __shared__ float s_max[8][32];
@@ -1239,9 +1252,11 @@ __global__ __launch_bounds__(kTileRows) void k_bias_boot(BiasHubArgs a) {
   for (int64_t h = blockIdx.x; h < H; h += gridDim.x) {
     const HubRowCtx c = hub_row_ctx(a, h, G, l);
     const int64_t ns = (c.deg + 31) / 32;
-    const int64_t s0 = ns * g / 8;
-    const int64_t s1 = ns >= 8 * kBiasSampleSteps ? s0 + kBiasSampleSteps : ns * (g + 1) / 8;
-    s_max[g][l] = sort32_desc(lane_max_run(c, s0, s1, l), l);
+    // 8 runs spread over the row, each up to kBiasSampleSteps draws (the whole row when it is
+    // shorter), cut at block boundaries
+    const int64_t s0 = ns * g / 8, s1 = ns * (g + 1) / 8;
+    const int64_t len = ns >= 8 * kBiasSampleSteps ? kBiasSampleSteps : s1 - s0 + 4;
+    s_max[g][l] = sort32_desc(lane_max_run(c, s0, s1, len, l), l);
     __syncthreads();
 #pragma unroll
     for (int step = 1; step < 8; step <<= 1) {
