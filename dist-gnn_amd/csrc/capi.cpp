@@ -608,9 +608,12 @@ int dgs_profile_enable(int mask) {
     // which-index bits: 0 = gather, 1 = sample, 2 = select (dgs_ops.h)
     int m = mask & 7;
     if (mask != 0 && (mask & ~7) != 0) m = 7;
+    // DGS_PROF_HUB=1 (diagnostics): the hub kernels' workgroup stamps ride along
+    static const bool hub = getenv("DGS_PROF_HUB") != nullptr;
+    if (hub && m) m |= 8 | 16;
     profiler().mask = m;
     profiler().on = m != 0;
-    if (m & 5) profile_reserve();  // gather or select stamps
+    if (m & 29) profile_reserve();  // gather, select or hub-kernel stamps
   });
 }
 

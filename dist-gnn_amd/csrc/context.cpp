@@ -324,6 +324,8 @@ void add_measure(int which, double ms) {
   } else if (which == 2) {
     profiler().select_ms += ms;
     profiler().select_n += 1;
+  } else if (which >= 3) {
+    // hub-kernel stamps: diagnostics only (printed by the detail report)
   } else {
     profiler().sample_ms += ms;
     profiler().sample_n += 1;
@@ -410,37 +412,44 @@ void profile_collect() {
     // DGS_PROF_DETAIL=1: per measurement, how a launch's span splits into the dispatch spread
     // (first to last workgroup start) and the workgroups' own durations (stderr, diagnostics)
     static const bool detail = getenv("DGS_PROF_DETAIL") != nullptr;
-    double d_span[3] = {0, 0, 0}, d_spread[3] = {0, 0, 0}, d_wg[3] = {0, 0, 0};
-    int64_t d_n[3] = {0, 0, 0};
+    // For the hub kernels (which 3 / 4, whose workgroups each own a fixed share of the work)
+    // also the end spread (first to last workgroup end) and the busy fraction (workgroup time
+    // over workgroups x span): a low fraction is time lost to late starts and uneven finishes.
+    constexpr int kW = 5;
+    double d_span[kW] = {}, d_spread[kW] = {}, d_wg[kW] = {}, d_end[kW] = {}, d_busy[kW] = {};
+    int64_t d_n[kW] = {};
     for (auto &r : sr) {
       h.resize((size_t)(2 * r.nblocks));
       DGS_HIP(hipMemcpy(h.data(), r.buf, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost));
-      uint64_t t0 = ~0ull, t1 = 0, s1 = 0;
+      uint64_t t0 = ~0ull, t1 = 0, s1 = 0, e0 = ~0ull;
       double wg = 0;
       for (int64_t b = 0; b < r.nblocks; ++b) {
         t0 = h[2 * b] < t0 ? h[2 * b] : t0;
         t1 = h[2 * b + 1] > t1 ? h[2 * b + 1] : t1;
         s1 = h[2 * b] > s1 ? h[2 * b] : s1;
+        e0 = h[2 * b + 1] < e0 ? h[2 * b + 1] : e0;
         wg += (double)(h[2 * b + 1] - h[2 * b]);
       }
       if (t1 > t0 && khz > 0) {
         add_measure(r.which, (double)(t1 - t0) / (double)khz);
-        if (detail && r.which >= 0 && r.which < 3) {
+        if (detail && r.which >= 0 && r.which < kW) {
           d_span[r.which] += (double)(t1 - t0) / khz;
           d_spread[r.which] += (double)(s1 - t0) / khz;
           d_wg[r.which] += wg / (double)r.nblocks / khz;
+          d_end[r.which] += (double)(t1 - e0) / khz;
+          d_busy[r.which] += wg / ((double)r.nblocks * (double)(t1 - t0));
           d_n[r.which] += 1;
         }
       }
       if (r.own) stamp_pool().push_back({r.nblocks, r.buf});
     }
-    for (int w = 0; detail && w < 3; ++w)
+    for (int w = 0; detail && w < kW; ++w)
       if (d_n[w])
         fprintf(stderr,
                 "[dgs prof] which=%d launches=%lld avg span %.2f us, dispatch spread %.2f us, "
-                "workgroup duration %.2f us\n",
+                "workgroup duration %.2f us, end spread %.2f us, busy %.3f\n",
                 w, (long long)d_n[w], 1e3 * d_span[w] / d_n[w], 1e3 * d_spread[w] / d_n[w],
-                1e3 * d_wg[w] / d_n[w]);
+                1e3 * d_wg[w] / d_n[w], 1e3 * d_end[w] / d_n[w], d_busy[w] / d_n[w]);
     sr.clear();
     stamp_slab().used = 0;
   }

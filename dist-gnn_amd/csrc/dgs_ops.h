@@ -155,7 +155,8 @@ struct Profiler {
 };
 Profiler &profiler();
 // which: 0 = feature-server gather kernel, 1 = multi-hop sample call (events before its
-// first and after its last kernel), 2 = plain index_select gather kernel.
+// first and after its last kernel), 2 = plain index_select gather kernel; diagnostics only
+// (DGS_PROF_HUB=1 with DGS_PROF_DETAIL=1, stderr): 3 = uniform hub reservoir, 4 = biased stream.
 // Kernel events: when profiling is on, returns (start, stop) events that hipExtLaunchKernelGGL
 // records at the kernel's own start / end; otherwise (null, null).
 struct KernelEvents {
