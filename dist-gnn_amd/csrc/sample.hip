@@ -1542,6 +1542,10 @@ __device__ __forceinline__ void merge_emit_at(const BiasHubArgs &a, int64_t S, i
 // ranges), merged in LDS.  The loads are grouped by dependence level (the list's header and the
 // row's output slot together, both candidate batches together, the next batch's entries under
 // the current batch's probabilities): this pass is latency-bound.
+#ifndef DGS_MERGE_ILP
+#define DGS_MERGE_ILP 4
+#endif
+constexpr int kMergeIlp = DGS_MERGE_ILP;
 __device__ __forceinline__ void stream_merge_block(const BiasHubArgs &a, int64_t blk,
                                                    int64_t nblk) {
   __shared__ float s_key[8][32];
@@ -1583,22 +1587,37 @@ __device__ __forceinline__ void stream_merge_block(const BiasHubArgs &a, int64_t
     } else {
       const int64_t cb = a.cand.base[h];
       const global_ptr<float> pr = as_global(reinterpret_cast<const float *>(a.hub.aux[h]));
-      int32_t e = 32 * g + l;
-      bool v = e < n;
-      int32_t idx = v ? a.cand.idx[cb + e] : INT32_MAX;
-      float u = v ? a.cand.key[cb + e] : 1.0f;
-      for (int32_t b0 = 32 * g; b0 < n; b0 += 256) {
-        const float p = v ? pr[idx] : 1.0f;
-        // the next batch's entries load under this batch's probabilities and keys
-        const int32_t en = e + 256;
-        const bool vn = en < n;
-        const int32_t idxn = vn ? a.cand.idx[cb + en] : INT32_MAX;
-        const float un = vn ? a.cand.key[cb + en] : 1.0f;
-        top.push(v ? ares_key(u, p) : -__builtin_inff(), idx, v, k, l);
-        e = en;
-        v = vn;
-        idx = idxn;
-        u = un;
+      // kMergeIlp batches per round: their entries load together, then their probabilities
+      // together, and the next round's entries load under this round's probabilities and keys
+      // (a long list's chain is its rounds' memory round trips)
+      int32_t idx[kMergeIlp];
+      float u[kMergeIlp];
+      auto load_round = [&](int32_t b0) {
+#pragma unroll
+        for (int j = 0; j < kMergeIlp; ++j) {
+          const int32_t e = b0 + 256 * j + l;
+          const bool v = e < n;
+          idx[j] = v ? a.cand.idx[cb + e] : INT32_MAX;
+          u[j] = v ? a.cand.key[cb + e] : 1.0f;
+        }
+      };
+      load_round(32 * g);
+      for (int32_t b0 = 32 * g; b0 < n; b0 += 256 * kMergeIlp) {
+        float p[kMergeIlp], uc[kMergeIlp];
+        int32_t ic[kMergeIlp];
+#pragma unroll
+        for (int j = 0; j < kMergeIlp; ++j) {
+          p[j] = idx[j] != INT32_MAX ? pr[idx[j]] : 1.0f;
+          ic[j] = idx[j];
+          uc[j] = u[j];
+        }
+        if (b0 + 256 * kMergeIlp < n) load_round(b0 + 256 * kMergeIlp);
+#pragma unroll
+        for (int j = 0; j < kMergeIlp; ++j) {
+          const bool v = ic[j] != INT32_MAX;
+          if (b0 + 256 * j >= n) break;  // (half-wave uniform)
+          top.push(v ? ares_key(uc[j], p[j]) : -__builtin_inff(), ic[j], v, k, l);
+        }
       }
     }
     tree_merge8(top, k, g, l, s_key, s_idx);
