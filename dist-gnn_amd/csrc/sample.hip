@@ -18,6 +18,7 @@
 //     RNG chain is recomputed from the degrees of the chain's earlier rows.
 // Offsets come from a reduce-then-scan over 256-row tiles (no host sync inside the hop).
 #include "dgs_block.cuh"
+#include "dgs_lane.cuh"
 #include "dgs_mod.cuh"
 #include "dgs_ops.h"
 #include "dgs_table.cuh"
@@ -712,8 +713,8 @@ struct HalfTopK {
   float thr_k = -__builtin_inff();
   int32_t thr_i = INT32_MAX;
   static __device__ __forceinline__ void cas(float &k, int32_t &i, int partner_mask, bool better_here) {
-    const float pk = __shfl_xor(k, partner_mask, 32);
-    const int32_t pi = __shfl_xor(i, partner_mask, 32);
+    const float pk = lane_xor32v(k, partner_mask);
+    const int32_t pi = lane_xor32v(i, partner_mask);
     const bool pb = ares_better(pk, pi, k, i);  // partner's entry is the better one
     if (better_here ? pb : !pb) {
       k = pk;
@@ -724,8 +725,8 @@ struct HalfTopK {
   // beat it are a prefix of length pos; the rest move down a lane (the 32nd drops out).
   __device__ __forceinline__ void insert_one(float ck, int32_t ci, int l) {
     const int pos = __builtin_popcount(half_ballot(ares_better(bk, bi, ck, ci)));
-    const float uk = __shfl_up(bk, 1, 32);
-    const int32_t ui = __shfl_up(bi, 1, 32);
+    const float uk = lane_up1_32(bk);
+    const int32_t ui = lane_up1_32(bi);
     if (l > pos) {
       bk = uk;
       bi = ui;
@@ -782,8 +783,8 @@ struct HalfTopK {
   // top 32 of the list and 32 candidates sorted descending: pairwise best against the
   // reversed candidates (a bitonic sequence), then a descending bitonic merge
   __device__ __forceinline__ void merge_sorted(float ck, int32_t ci, int64_t k, int l) {
-    const float rk = __shfl(ck, 31 - l, 32);
-    const int32_t ri = __shfl(ci, 31 - l, 32);
+    const float rk = lane_rev32(ck);
+    const int32_t ri = lane_rev32(ci);
     if (ares_better(rk, ri, bk, bi)) {
       bk = rk;
       bi = ri;
@@ -794,8 +795,8 @@ struct HalfTopK {
   }
   __device__ __forceinline__ void update_thr(int64_t k, int l) {
     cnt = __builtin_popcount(half_ballot(l < k && bi != INT32_MAX));
-    thr_k = __shfl(bk, (int)(k - 1), 32);
-    thr_i = __shfl(bi, (int)(k - 1), 32);
+    thr_k = half_bcast(bk, (int)(k - 1));
+    thr_i = half_bcast(bi, (int)(k - 1));
   }
   // true once k entries are held and the threshold is finite (ares_may_pass is then valid)
   __device__ __forceinline__ bool filtering(int64_t k) const {
@@ -1275,7 +1276,7 @@ __device__ __forceinline__ float sort32_desc(float v, int l) {
   for (int size = 2; size <= 32; size <<= 1) {
 #pragma unroll
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const float o = __shfl_xor(v, stride, 32);
+      const float o = lane_xor32v(v, stride);
       const bool desc = (l & size) == 0 || size == 32;
       const bool lower = (l & stride) == 0;
       v = (desc == lower) ? fmaxf(v, o) : fminf(v, o);
@@ -1313,7 +1314,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_boot(BiasHubArgs a) {
         float v = fmaxf(s_max[g][l], s_max[g + step][31 - l]);
 #pragma unroll
         for (int stride = 16; stride > 0; stride >>= 1) {
-          const float o = __shfl_xor(v, stride, 32);
+          const float o = lane_xor32v(v, stride);
           v = (l & stride) == 0 ? fmaxf(v, o) : fminf(v, o);
         }
         s_max[g][l] = v;

@@ -1,0 +1,63 @@
+// Checks the half-wave lane moves of dist-gnn_amd/csrc/dgs_lane.cuh against HIP's __shfl forms
+// on the GPU: every helper, with the whole wave active and with only one half active.
+//   hipcc --offload-arch=gfx950 -O3 -I dist-gnn_amd/csrc tools/lane_ops_test.hip -o tools/lane_ops_test
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "dgs_lane.cuh"
+
+using namespace dgs;
+
+// out[t * 64 + lane]: mismatch flags of test t (0 = equal)
+__global__ void k_lane_test(const int32_t *in, int32_t *bad, int mode, int q) {
+  const int lane = threadIdx.x;
+  const int32_t x = in[blockIdx.x * 64 + lane];
+  const bool active = mode == 0 || (mode == 1 && lane < 32) || (mode == 2 && lane >= 32);
+  if (!active) return;
+  int32_t *b = bad + (size_t)blockIdx.x * 8 * 64;
+  const int l = lane & 31;
+  b[0 * 64 + lane] = lane_xor32<1>(x) != __shfl_xor(x, 1, 32);
+  b[1 * 64 + lane] = lane_xor32<2>(x) != __shfl_xor(x, 2, 32);
+  b[2 * 64 + lane] = lane_xor32<4>(x) != __shfl_xor(x, 4, 32);
+  b[3 * 64 + lane] = lane_xor32<8>(x) != __shfl_xor(x, 8, 32);
+  b[4 * 64 + lane] = lane_xor32<16>(x) != __shfl_xor(x, 16, 32);
+  b[5 * 64 + lane] = lane_rev32(x) != __shfl(x, 31 - l, 32);
+  b[6 * 64 + lane] = l > 0 && lane_up1_32(x) != __shfl_up(x, 1, 32);
+  b[7 * 64 + lane] = half_bcast(x, q) != __shfl(x, q, 32);
+}
+
+int main() {
+  const int nb = 64;
+  int32_t *h = (int32_t *)malloc(sizeof(int32_t) * nb * 64);
+  srand(7);
+  for (int i = 0; i < nb * 64; ++i) h[i] = rand() ^ (rand() << 16);
+  int32_t *din, *dbad;
+  hipMalloc(&din, sizeof(int32_t) * nb * 64);
+  hipMalloc(&dbad, sizeof(int32_t) * nb * 8 * 64);
+  hipMemcpy(din, h, sizeof(int32_t) * nb * 64, hipMemcpyHostToDevice);
+  int32_t *hb = (int32_t *)malloc(sizeof(int32_t) * nb * 8 * 64);
+  const char *names[8] = {"xor1", "xor2", "xor4", "xor8", "xor16", "rev32", "up1", "bcast"};
+  int total = 0;
+  for (int mode = 0; mode < 3; ++mode) {
+    for (int q = 0; q < 32; q += 13) {
+      hipMemset(dbad, 0, sizeof(int32_t) * nb * 8 * 64);
+      hipLaunchKernelGGL(k_lane_test, dim3(nb), dim3(64), 0, 0, din, dbad, mode, q);
+      if (hipDeviceSynchronize() != hipSuccess) {
+        printf("kernel failed\n");
+        return 2;
+      }
+      hipMemcpy(hb, dbad, sizeof(int32_t) * nb * 8 * 64, hipMemcpyDeviceToHost);
+      for (int t = 0; t < 8; ++t) {
+        int n = 0;
+        for (int blk = 0; blk < nb; ++blk)
+          for (int lane = 0; lane < 64; ++lane) n += hb[(blk * 8 + t) * 64 + lane] != 0;
+        if (n) printf("mode %d q %d %s: %d mismatches\n", mode, q, names[t], n);
+        total += n;
+      }
+    }
+  }
+  printf("lane ops: %s (%d mismatches)\n", total ? "FAIL" : "ok", total);
+  return total ? 1 : 0;
+}
