@@ -882,12 +882,51 @@ __device__ __forceinline__ void sample_bias_block(
 #pragma unroll
         for (int e = 0; e < 5; ++e) w2[e] = bitsel(m2, wv[e + 2], wv[e]);
         float u[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) u[s4] = curand_uniform_from(bitsel(m1, w2[s4 + 1], w2[s4]));
+        if (!filter) {
+          // No threshold yet (a row's first group): every edge is a candidate.  The lane's 4
+          // exact keys are sorted in registers and pushed best first, so only the first push is
+          // a full 32-candidate merge and the later ones meet the threshold it set (mostly
+          // sparse inserts) -- the same list as any order.
+          float kq[4];
+          int32_t iq[4];
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const int32_t i = (int32_t)(128 * g + 32 * s4 + l);
+            const bool valid = i < deg;
+            kq[s4] = valid ? ares_key(u[s4], p[s4]) : -__builtin_inff();
+            iq[s4] = valid ? i : INT32_MAX;
+          }
+          auto cswap = [&](int x, int y) {
+            if (ares_better(kq[y], iq[y], kq[x], iq[x])) {
+              const float tk = kq[x];
+              const int32_t ti = iq[x];
+              kq[x] = kq[y];
+              iq[x] = iq[y];
+              kq[y] = tk;
+              iq[y] = ti;
+            }
+          };
+          cswap(0, 1);
+          cswap(2, 3);
+          cswap(0, 2);
+          cswap(1, 3);
+          cswap(1, 2);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) top.push(kq[q], iq[q], iq[q] != INT32_MAX, k, l);
+          if (top.filtering(k)) {
+            filter = true;
+            thr_s = slack_thr(top.thr_k);
+          }
+          A = B;
+          continue;
+        }
         uint32_t mk = 0;
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
-          u[s4] = curand_uniform_from(bitsel(m1, w2[s4 + 1], w2[s4]));
           const bool valid = 128 * g + 32 * s4 + l < deg;
-          mk |= (uint32_t)(valid & (!filter | ares_may_pass_s(u[s4], p[s4], thr_s))) << s4;
+          mk |= (uint32_t)(valid & ares_may_pass_s(u[s4], p[s4], thr_s)) << s4;
         }
         // candidates in rounds of one per lane (the resulting list does not depend on order)
         while (half_ballot(mk != 0)) {
