@@ -12,9 +12,11 @@
 //               of the other: with both operands x, row 2j reads row 2j + 1 from the second
 //               result and row 2j + 1 reads row 2j from the first)
 //   31 - l      row_mirror (15 - l inside each row), then xor 16
-//   l - 1       row_shr:1 inside each row; lane 16 of each half takes lane 15 by a scalar read
+//   l - 1       row_shr:1 inside each row; lane 16 of each half takes lane 15 from the reversal
+//               (branch-free: a select between readlanes of lanes 15 and 47 compiles to a branch)
 // Every helper reads lanes of the caller's own half only, so it is safe when the two halves of a
-// wave follow different control flow (each half is either wholly active or wholly inactive).
+// wave follow different control flow, but each half must be wholly active: a DPP move that reads
+// a lane whose exec bit is clear does not see that lane's value.
 // tools/lane_ops_test.hip checks each helper against the __shfl form on the GPU.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -76,8 +78,7 @@ __device__ __forceinline__ float lane_rev32(float x) {
 // x of lane l - 1 of this half (lane 0 of the half: its own x; callers ignore it).
 __device__ __forceinline__ int32_t lane_up1_32(int32_t x) {
   const int32_t t = dpp_keep<0x111>(x, x);  // row_shr:1 (lane 0 of a row keeps x)
-  const int32_t b = (threadIdx.x & 32) ? __builtin_amdgcn_readlane(x, 47)
-                                       : __builtin_amdgcn_readlane(x, 15);
+  const int32_t b = lane_rev32(x);           // at lane 16: lane 15
   return (threadIdx.x & 31) == 16 ? b : t;
 }
 __device__ __forceinline__ float lane_up1_32(float x) {
