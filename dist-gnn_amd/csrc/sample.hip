@@ -63,6 +63,19 @@ int hub_dyn() {
   return n;
 }
 
+// Sixteenths of the streamed chunks k_bias_stream's workers draw dynamically; DGS_BIAS_DYN
+// overrides (0: a fixed share per worker).
+constexpr int kBiasDyn = 0;
+constexpr uint32_t kBiasGrab = 4;
+int bias_dyn() {
+  static const int n = [] {
+    const char *e = getenv("DGS_BIAS_DYN");
+    const int v = e ? atoi(e) : -1;
+    return v >= 0 && v <= 16 ? v : kBiasDyn;
+  }();
+  return n;
+}
+
 constexpr int kBiasStreamBlocks = 768;  // round 3 A/B: 512-768 best, 1024 -1.5 %, 1536 -9 %
 // Workgroups of the streaming kernel; DGS_BIAS_STREAM_BLOCKS overrides.
 int bias_stream_blocks() {
@@ -1370,7 +1383,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_boot(BiasHubArgs a) {
 // kept in 32 bits (a row has < 2^31 edges, a lane's draw offset < 2^28, the hop's chunk count
 // and candidate room < 2^31): register pressure, not arithmetic, sets this kernel's occupancy.
 __device__ __forceinline__ void bias_stream_body(const BiasHubArgs &a, const int64_t *bsum,
-                                                 int64_t *boff, int64_t *d_nnz) {
+                                                 int64_t *boff, int64_t *d_nnz, int dyn) {
   if (blockIdx.x == 0) {
     __shared__ int64_t lds[kTileRows / 64];
     const int64_t nb = (a.Sc.get() + kTileRows - 1) / kTileRows;
@@ -1390,10 +1403,17 @@ __device__ __forceinline__ void bias_stream_body(const BiasHubArgs &a, const int
   const int64_t wk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 5;
   const int64_t nw = bias_workers(total, a.nworkers);
   if (wk >= nw) return;
-  const uint32_t c0 = (uint32_t)bias_worker_c0(total, wk, nw);
-  const uint32_t c1 = (uint32_t)bias_worker_c0(total, wk + 1, nw);
-  if (c0 >= c1) return;
-  int64_t h = group_search<32>(a.hub.cptr, H, c0);
+  // The first total - D chunks in a fixed share per worker; the last D = total * dyn / 16 in 8
+  // pools (pool x: workgroups with blockIdx mod 8 = x, one XCD each under the round-robin
+  // dispatch) that workers draw kBiasGrab-chunk ranges from once their share is done (as in
+  // k_hub_reservoir).  Pools need workers in every x: none below 64 workers.
+  const int64_t D = nw >= 64 ? total * dyn / 16 : 0, Ts = total - D;
+  uint32_t c0 = (uint32_t)bias_worker_c0(Ts, wk, nw);
+  uint32_t c1 = (uint32_t)bias_worker_c0(Ts, wk + 1, nw);
+  const int px = blockIdx.x & 7;
+  const uint32_t p0 = (uint32_t)(Ts + D * px / 8), p1 = (uint32_t)(Ts + D * (px + 1) / 8);
+  if (c0 >= c1 && p0 >= p1) return;
+  int64_t h = 0;
   uint32_t hstart = 0, hnext = 0, deg = 0, jb = 0, off = 0, sub = 0;
   global_ptr<float> pr = nullptr;
   PhiloxKeys kk;
@@ -1481,74 +1501,88 @@ __device__ __forceinline__ void bias_stream_body(const BiasHubArgs &a, const int
     __builtin_amdgcn_wave_barrier();
     nb = 0;
   };
-  load_row(h);
   // the next chunk's probabilities, loaded under this chunk's Philox (same row only)
   float pn[kStreamT];
-  bool have_next = false;
-  for (uint32_t ch = c0; ch < c1; ++ch) {
-    while (ch >= hnext) {
-      ++h;
+  for (;;) {
+    if (c0 < c1) {
+      h += group_search<32>(a.hub.cptr + h, H - h, c0);  // ranges only move forward
       load_row(h);
-    }
-    if (skip) continue;
-    const uint32_t q = ch - hstart;
-    const int32_t i0 = chunk_i0(q);
-    const bool whole = chunk_whole(i0);
-    if (!have_next) load_probs(q, pn);
-    float p[kStreamT];
+      bool have_next = false;
+      for (uint32_t ch = c0; ch < c1; ++ch) {
+        while (ch >= hnext) {
+          ++h;
+          load_row(h);
+        }
+        if (skip) continue;
+        const uint32_t q = ch - hstart;
+        const int32_t i0 = chunk_i0(q);
+        const bool whole = chunk_whole(i0);
+        if (!have_next) load_probs(q, pn);
+        float p[kStreamT];
 #pragma unroll
-    for (int t = 0; t < kStreamT; ++t) p[t] = pn[t];
-    have_next = ch + 1 < c1 && ch + 1 < hnext;
-    if (have_next) load_probs(q + 1, pn);
-    const uint32_t bc = (jb >> 2) + q * (kStreamT / 4);
-    uint32_t xs[kStreamT];
+        for (int t = 0; t < kStreamT; ++t) p[t] = pn[t];
+        have_next = ch + 1 < c1 && ch + 1 < hnext;
+        if (have_next) load_probs(q + 1, pn);
+        const uint32_t bc = (jb >> 2) + q * (kStreamT / 4);
+        uint32_t xs[kStreamT];
 #pragma unroll
-    for (int bq = 0; bq < kStreamT / 4; ++bq) {
-      const uint4 o = philox4x32_10(make_uint4(bc + bq, 0u, sub, 0u), kk);
-      xs[4 * bq + 0] = o.x;
-      xs[4 * bq + 1] = o.y;
-      xs[4 * bq + 2] = o.z;
-      xs[4 * bq + 3] = o.w;
-    }
-    // Per step t, the wave's lanes whose edge passes the cheap bound, straight from the compares
-    // (lin_pass_mask: one convert, one fma and one compare per edge; round 3 A/B against the
-    // hardware-log2 bound: +1.7 %); the valid-edge compare only matters in a row's first and
-    // last chunks.
-    uint64_t pass[kStreamT];
+        for (int bq = 0; bq < kStreamT / 4; ++bq) {
+          const uint4 o = philox4x32_10(make_uint4(bc + bq, 0u, sub, 0u), kk);
+          xs[4 * bq + 0] = o.x;
+          xs[4 * bq + 1] = o.y;
+          xs[4 * bq + 2] = o.z;
+          xs[4 * bq + 3] = o.w;
+        }
+        // Per step t, the wave's lanes whose edge passes the cheap bound, straight from the
+        // compares (lin_pass_mask: one convert, one fma and one compare per edge; round 3 A/B
+        // against the hardware-log2 bound: +1.7 %); the valid-edge compare only matters in a
+        // row's first and last chunks.
+        uint64_t pass[kStreamT];
 #pragma unroll
-    for (int t = 0; t < kStreamT; ++t) pass[t] = lin_pass_mask(xs[t], p[t], cx);
-    const uint64_t whole_mask = __ballot(whole);
-    if (whole_mask != __builtin_amdgcn_read_exec()) {  // (wave-uniform: a row's first / last chunk)
+        for (int t = 0; t < kStreamT; ++t) pass[t] = lin_pass_mask(xs[t], p[t], cx);
+        const uint64_t whole_mask = __ballot(whole);
+        // (wave-uniform: a row's first / last chunk)
+        if (whole_mask != __builtin_amdgcn_read_exec()) {
 #pragma unroll
-      for (int t = 0; t < kStreamT; ++t)  // (a negative edge compares as a huge unsigned one)
-        pass[t] &= whole_mask | __builtin_amdgcn_uicmp((uint32_t)(i0 + 32 * t), deg, 36 /*ULT*/);
-    }
-    // the few that pass go to the list as (draw, edge); the merge computes their exact keys
-    // (keeping the fixed-operation key out of this loop saves registers)
-    if (nb > kStreamBuf - kStreamChunk) flush();
-    const int hs = threadIdx.x & 32;
+          for (int t = 0; t < kStreamT; ++t)  // (a negative edge compares as a huge unsigned one)
+            pass[t] &= whole_mask |
+                       __builtin_amdgcn_uicmp((uint32_t)(i0 + 32 * t), deg, 36 /*ULT*/);
+        }
+        // the few that pass go to the list as (draw, edge); the merge computes their exact keys
+        // (keeping the fixed-operation key out of this loop saves registers)
+        if (nb > kStreamBuf - kStreamChunk) flush();
+        const int hs = threadIdx.x & 32;
 #pragma unroll
-    for (int t = 0; t < kStreamT; ++t) {
-      if (pass[t] == 0) continue;
-      const uint32_t b = (uint32_t)(pass[t] >> hs);
-      if ((b >> l) & 1u) {
-        const int pos = nb + __builtin_popcount(b & ((1u << l) - 1u));
-        s_x[g][pos] = xs[t];
-        s_i[g][pos] = (uint32_t)(i0 + 32 * t);
-        s_h[g][pos] = (int32_t)h;
+        for (int t = 0; t < kStreamT; ++t) {
+          if (pass[t] == 0) continue;
+          const uint32_t b = (uint32_t)(pass[t] >> hs);
+          if ((b >> l) & 1u) {
+            const int pos = nb + __builtin_popcount(b & ((1u << l) - 1u));
+            s_x[g][pos] = xs[t];
+            s_i[g][pos] = (uint32_t)(i0 + 32 * t);
+            s_h[g][pos] = (int32_t)h;
+          }
+          nb += __builtin_popcount(b);
+        }
       }
-      nb += __builtin_popcount(b);
     }
+    if (p0 >= p1) break;
+    uint32_t gr = 0;
+    if (l == 0) gr = (uint32_t)atomicAdd((unsigned long long *)(a.hub.count + 8 + px),
+                                         (unsigned long long)kBiasGrab);
+    c0 = p0 + (uint32_t)__shfl((int32_t)gr, 0, 32);
+    if (c0 >= p1) break;
+    c1 = c0 + kBiasGrab < p1 ? c0 + kBiasGrab : p1;
   }
   if (nb > 0) flush();
 }
 
 __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const int64_t *bsum,
                                                            int64_t *boff, int64_t *d_nnz,
-                                                           uint64_t *stamp) {
+                                                           uint64_t *stamp, int dyn) {
   // profiling only (DGS_PROF_HUB: stamp != nullptr, a kernel argument: uniform branch)
   if (stamp && threadIdx.x == 0) stamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-  bias_stream_body(a, bsum, boff, d_nnz);
+  bias_stream_body(a, bsum, boff, d_nnz, dyn);
   if (stamp) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1860,7 +1894,7 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
       // (its workgroup 0 also does the hop's tile-offset scan)
       hipLaunchKernelGGL(k_bias_stream, dim3(bias_stream_blocks()), dim3(kTileRows), 0, st, ba,
                          (const int64_t *)bsum, boff, d_nnz,
-                         profile_stamps(4, bias_stream_blocks()));
+                         profile_stamps(4, bias_stream_blocks()), bias_dyn());
       DGS_LAUNCH_CHECK();
       if (stats) {  // candidates per hub row after the stream
         DGS_HIP(hipStreamSynchronize(st));

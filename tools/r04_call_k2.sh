@@ -18,3 +18,12 @@ AB_ROUNDS=3 AB_VARIANTS="ab/pre/libdgs_amd.so $L $L,DGS_HUB_DYN=4 $L,DGS_HUB_DYN
 if [ $lrc -eq 0 ] && [ ${prc:-1} -eq 0 ]; then
   AB_ROUNDS=3 AB_VARIANTS="ab/ilp4/libdgs_amd.so $L" AB_ARGS="--bias" bash tools/r04_run.sh r04_k2_biasab ab
 fi
+# biased stream kernel with dynamic pools (ab/bdyn = HEAD + pools in k_bias_stream, DGS_BIAS_DYN)
+DGS_AMD_LIB=$PWD/ab/bdyn/libdgs_amd.so DGS_BIAS_DYN=8 timeout -k 10 600 python -u -m pytest \
+  tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k bias \
+  > $O/pytest_bdyn8.log 2>&1; brc=$?; tail -2 $O/pytest_bdyn8.log; case $brc in 0|1) ;; *) exit $brc ;; esac
+if [ $brc -eq 0 ]; then
+  B=ab/bdyn/libdgs_amd.so
+  AB_ROUNDS=3 AB_VARIANTS="$B $B,DGS_BIAS_DYN=4 $B,DGS_BIAS_DYN=8" AB_ARGS="--bias" \
+    bash tools/r04_run.sh r04_k2_bdynab ab
+fi
