@@ -10,6 +10,14 @@
 
 using namespace dgs;
 
+#define CHECK(x)                                          \
+  do {                                                    \
+    if ((x) != hipSuccess) {                              \
+      printf("%s failed\n", #x);                          \
+      exit(2);                                            \
+    }                                                     \
+  } while (0)
+
 // out[t * 64 + lane]: mismatch flags of test t (0 = equal)
 __global__ void k_lane_test(const int32_t *in, int32_t *bad, int mode, int q) {
   const int lane = threadIdx.x;
@@ -43,22 +51,22 @@ int main() {
   srand(7);
   for (int i = 0; i < nb * 64; ++i) h[i] = rand() ^ (rand() << 16);
   int32_t *din, *dbad;
-  hipMalloc(&din, sizeof(int32_t) * nb * 64);
-  hipMalloc(&dbad, sizeof(int32_t) * nb * 9 * 64);
-  hipMemcpy(din, h, sizeof(int32_t) * nb * 64, hipMemcpyHostToDevice);
+  CHECK(hipMalloc(&din, sizeof(int32_t) * nb * 64));
+  CHECK(hipMalloc(&dbad, sizeof(int32_t) * nb * 9 * 64));
+  CHECK(hipMemcpy(din, h, sizeof(int32_t) * nb * 64, hipMemcpyHostToDevice));
   int32_t *hb = (int32_t *)malloc(sizeof(int32_t) * nb * 9 * 64);
   const char *names[9] = {"xor1", "xor2", "xor4", "xor8", "xor16", "rev32", "up1", "bcast",
                           "(wave_shr1)"};
   int total = 0;
   for (int mode = 0; mode < 3; ++mode) {
     for (int q = 0; q < 32; q += 13) {
-      hipMemset(dbad, 0, sizeof(int32_t) * nb * 9 * 64);
+      CHECK(hipMemset(dbad, 0, sizeof(int32_t) * nb * 9 * 64));
       hipLaunchKernelGGL(k_lane_test, dim3(nb), dim3(64), 0, 0, din, dbad, mode, q);
       if (hipDeviceSynchronize() != hipSuccess) {
         printf("kernel failed\n");
         return 2;
       }
-      hipMemcpy(hb, dbad, sizeof(int32_t) * nb * 9 * 64, hipMemcpyDeviceToHost);
+      CHECK(hipMemcpy(hb, dbad, sizeof(int32_t) * nb * 9 * 64, hipMemcpyDeviceToHost));
       for (int t = 0; t < 9; ++t) {
         int n = 0, first = -1;
         for (int blk = 0; blk < nb; ++blk)
