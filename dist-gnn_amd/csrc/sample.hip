@@ -51,31 +51,6 @@ int hub_blocks() {
   return n;
 }
 
-// Sixteenths of the hub chunks the uniform hub kernel's waves draw dynamically (k_hub_reservoir);
-// DGS_HUB_DYN overrides (0: a fixed share per wave).
-constexpr int kHubDyn = 0;
-int hub_dyn() {
-  static const int n = [] {
-    const char *e = getenv("DGS_HUB_DYN");
-    const int v = e ? atoi(e) : -1;
-    return v >= 0 && v <= 16 ? v : kHubDyn;
-  }();
-  return n;
-}
-
-// Sixteenths of the streamed chunks k_bias_stream's workers draw dynamically; DGS_BIAS_DYN
-// overrides (0: a fixed share per worker).
-constexpr int kBiasDyn = 0;
-constexpr uint32_t kBiasGrab = 4;
-int bias_dyn() {
-  static const int n = [] {
-    const char *e = getenv("DGS_BIAS_DYN");
-    const int v = e ? atoi(e) : -1;
-    return v >= 0 && v <= 16 ? v : kBiasDyn;
-  }();
-  return n;
-}
-
 constexpr int kBiasStreamBlocks = 768;  // round 3 A/B: 512-768 best, 1024 -1.5 %, 1536 -9 %
 // Workgroups of the streaming kernel; DGS_BIAS_STREAM_BLOCKS overrides.
 int bias_stream_blocks() {
@@ -257,8 +232,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, int64_t blk) {
   const int64_t S = a.Sc.get();
   const int64_t k = a.k;
   // the next hop's counter was last used two hops ago: reset it here (no memset launch)
-  // (and its pool counters, words 8-15 of its group)
-  if (blk == 0 && threadIdx.x < 9) a.next_hub_count[threadIdx.x ? 7 + threadIdx.x : 0] = 0;
+  if (blk == 0 && threadIdx.x == 0) *a.next_hub_count = 0;
   if (blk * kTileRows >= S) return;  // whole workgroup past the live rows
   const int64_t i = blk * kTileRows + threadIdx.x;
   int64_t cnt = 0, tdeg = 0;
@@ -420,16 +394,20 @@ __device__ __forceinline__ void hub_chunk32(const uint4 &o4a, const uint4 &o4b, 
 // (idx = k + 512q + t + 128w, t < 128, w < 4 <-> one Philox block per logical thread t) of the
 // hub rows and folds their picks into the rows' k global slots with atomicMax
 // (rowwise_sampling.cu:85-92; any split gives the same maxima).
-// Chunks [c0, c1) of the hub rows (the row of c0 is searched in [hlo, H)); returns the row of
-// the range's last chunk.
-__device__ __forceinline__ int64_t hub_range(const UniformArgs &a, int64_t S, int64_t H,
-                                             int64_t total, int64_t c0, int64_t c1, int64_t hlo) {
+__device__ __forceinline__ void hub_reservoir(const UniformArgs &a, int64_t gw, int64_t nwaves) {
+  const int64_t S = a.Sc.get();
   const int64_t k = a.k;
   const HubView &hub = a.hub;
+  const uint64_t packed = (uint64_t)*hub.count;
+  const int64_t H = (int64_t)(packed >> kHubShift);
+  if (H == 0) return;
+  const int64_t total = (int64_t)(packed & kHubChunkMask);
   const int lane = threadIdx.x & 63;
-  // One search per range, then the hub index only moves forward (a dependent search per chunk
-  // would dominate the Philox work).
-  int64_t h = hlo + group_search<64>(hub.cptr + hlo, H - hlo, c0);  // largest h: cptr[h] <= c0
+  // One binary search per wave, then the hub index only moves forward (a dependent search per
+  // chunk would dominate the Philox work).
+  const int64_t c0 = total * gw / nwaves, c1 = total * (gw + 1) / nwaves;
+  if (c0 >= c1) return;
+  int64_t h = group_search<64>(hub.cptr, H, c0);  // largest h with cptr[h] <= c0
   int64_t hstart = hub.cptr[h], hnext = h + 1 < H ? hub.cptr[h + 1] : total;
   // per-row values, made wave-uniform once per row (scalar key and slot address: nothing of
   // the row is recomputed per chunk)
@@ -486,37 +464,6 @@ __device__ __forceinline__ int64_t hub_range(const UniformArgs &a, int64_t S, in
         }
       }
     }
-  }
-  return h;
-}
-
-// Hub reservoir: wave gw of nwaves takes a contiguous share of the first total - D chunks; the
-// last D = total * dyn / 16 chunks form 8 pools (pool x: workgroups with blockIdx mod 8 = x, one
-// XCD each under the round-robin dispatch) that the waves draw kHubGrab-chunk ranges from with a
-// returning atomic once their share is done, so a wave that started late or shared its SIMD with
-// other kernels' waves does not set the kernel's end.  Any split gives the same maxima.
-constexpr int64_t kHubGrab = 2;
-__device__ __forceinline__ void hub_reservoir(const UniformArgs &a, int64_t gw, int64_t nwaves,
-                                              int dyn) {
-  const int64_t S = a.Sc.get();
-  const HubView &hub = a.hub;
-  const uint64_t packed = (uint64_t)*hub.count;
-  const int64_t H = (int64_t)(packed >> kHubShift);
-  if (H == 0) return;
-  const int64_t total = (int64_t)(packed & kHubChunkMask);
-  const int64_t D = total * dyn / 16, Ts = total - D;
-  int64_t c0 = Ts * gw / nwaves, c1 = Ts * (gw + 1) / nwaves, hlo = 0;
-  const int x = blockIdx.x & 7;
-  const int64_t p0 = Ts + D * x / 8, p1 = Ts + D * (x + 1) / 8;
-  for (;;) {
-    if (c0 < c1) hlo = hub_range(a, S, H, total, c0, c1, hlo);
-    if (p0 >= p1) return;
-    uint64_t g = 0;
-    if ((threadIdx.x & 63) == 0)
-      g = atomicAdd((unsigned long long *)(hub.count + 8 + x), (unsigned long long)kHubGrab);
-    c0 = p0 + (int64_t)wave_uniform(__shfl(g, 0));
-    if (c0 >= p1) return;
-    c1 = c0 + kHubGrab < p1 ? c0 + kHubGrab : p1;
   }
 }
 
@@ -599,7 +546,7 @@ __device__ __forceinline__ void sample_rows(const UniformArgs &a, int64_t blk, i
 // launch fewer per hop.
 __global__ __launch_bounds__(256) void k_hub_reservoir(UniformArgs a, const int64_t *bsum,
                                                        int64_t *boff, int64_t *d_nnz,
-                                                       uint64_t *stamp, int dyn) {
+                                                       uint64_t *stamp) {
   // profiling only (DGS_PROF_HUB: stamp != nullptr, a kernel argument: uniform branch)
   if (stamp && threadIdx.x == 0) stamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   if (blockIdx.x == 0) {
@@ -616,7 +563,7 @@ __global__ __launch_bounds__(256) void k_hub_reservoir(UniformArgs a, const int6
   // second round's M1 product of both Philox blocks of a chunk
   const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) +
                      __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  hub_reservoir(a, gw, ((int64_t)gridDim.x * blockDim.x) >> 6, dyn);
+  hub_reservoir(a, gw, ((int64_t)gridDim.x * blockDim.x) >> 6);
   if (stamp) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1383,7 +1330,7 @@ __global__ __launch_bounds__(kTileRows) void k_bias_boot(BiasHubArgs a) {
 // kept in 32 bits (a row has < 2^31 edges, a lane's draw offset < 2^28, the hop's chunk count
 // and candidate room < 2^31): register pressure, not arithmetic, sets this kernel's occupancy.
 __device__ __forceinline__ void bias_stream_body(const BiasHubArgs &a, const int64_t *bsum,
-                                                 int64_t *boff, int64_t *d_nnz, int dyn) {
+                                                 int64_t *boff, int64_t *d_nnz) {
   if (blockIdx.x == 0) {
     __shared__ int64_t lds[kTileRows / 64];
     const int64_t nb = (a.Sc.get() + kTileRows - 1) / kTileRows;
@@ -1403,17 +1350,10 @@ __device__ __forceinline__ void bias_stream_body(const BiasHubArgs &a, const int
   const int64_t wk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 5;
   const int64_t nw = bias_workers(total, a.nworkers);
   if (wk >= nw) return;
-  // The first total - D chunks in a fixed share per worker; the last D = total * dyn / 16 in 8
-  // pools (pool x: workgroups with blockIdx mod 8 = x, one XCD each under the round-robin
-  // dispatch) that workers draw kBiasGrab-chunk ranges from once their share is done (as in
-  // k_hub_reservoir).  Pools need workers in every x: none below 64 workers.
-  const int64_t D = nw >= 64 ? total * dyn / 16 : 0, Ts = total - D;
-  uint32_t c0 = (uint32_t)bias_worker_c0(Ts, wk, nw);
-  uint32_t c1 = (uint32_t)bias_worker_c0(Ts, wk + 1, nw);
-  const int px = blockIdx.x & 7;
-  const uint32_t p0 = (uint32_t)(Ts + D * px / 8), p1 = (uint32_t)(Ts + D * (px + 1) / 8);
-  if (c0 >= c1 && p0 >= p1) return;
-  int64_t h = 0;
+  const uint32_t c0 = (uint32_t)bias_worker_c0(total, wk, nw);
+  const uint32_t c1 = (uint32_t)bias_worker_c0(total, wk + 1, nw);
+  if (c0 >= c1) return;
+  int64_t h = group_search<32>(a.hub.cptr, H, c0);
   uint32_t hstart = 0, hnext = 0, deg = 0, jb = 0, off = 0, sub = 0;
   global_ptr<float> pr = nullptr;
   PhiloxKeys kk;
@@ -1501,88 +1441,74 @@ __device__ __forceinline__ void bias_stream_body(const BiasHubArgs &a, const int
     __builtin_amdgcn_wave_barrier();
     nb = 0;
   };
+  load_row(h);
   // the next chunk's probabilities, loaded under this chunk's Philox (same row only)
   float pn[kStreamT];
-  for (;;) {
-    if (c0 < c1) {
-      h += group_search<32>(a.hub.cptr + h, H - h, c0);  // ranges only move forward
+  bool have_next = false;
+  for (uint32_t ch = c0; ch < c1; ++ch) {
+    while (ch >= hnext) {
+      ++h;
       load_row(h);
-      bool have_next = false;
-      for (uint32_t ch = c0; ch < c1; ++ch) {
-        while (ch >= hnext) {
-          ++h;
-          load_row(h);
-        }
-        if (skip) continue;
-        const uint32_t q = ch - hstart;
-        const int32_t i0 = chunk_i0(q);
-        const bool whole = chunk_whole(i0);
-        if (!have_next) load_probs(q, pn);
-        float p[kStreamT];
-#pragma unroll
-        for (int t = 0; t < kStreamT; ++t) p[t] = pn[t];
-        have_next = ch + 1 < c1 && ch + 1 < hnext;
-        if (have_next) load_probs(q + 1, pn);
-        const uint32_t bc = (jb >> 2) + q * (kStreamT / 4);
-        uint32_t xs[kStreamT];
-#pragma unroll
-        for (int bq = 0; bq < kStreamT / 4; ++bq) {
-          const uint4 o = philox4x32_10(make_uint4(bc + bq, 0u, sub, 0u), kk);
-          xs[4 * bq + 0] = o.x;
-          xs[4 * bq + 1] = o.y;
-          xs[4 * bq + 2] = o.z;
-          xs[4 * bq + 3] = o.w;
-        }
-        // Per step t, the wave's lanes whose edge passes the cheap bound, straight from the
-        // compares (lin_pass_mask: one convert, one fma and one compare per edge; round 3 A/B
-        // against the hardware-log2 bound: +1.7 %); the valid-edge compare only matters in a
-        // row's first and last chunks.
-        uint64_t pass[kStreamT];
-#pragma unroll
-        for (int t = 0; t < kStreamT; ++t) pass[t] = lin_pass_mask(xs[t], p[t], cx);
-        const uint64_t whole_mask = __ballot(whole);
-        // (wave-uniform: a row's first / last chunk)
-        if (whole_mask != __builtin_amdgcn_read_exec()) {
-#pragma unroll
-          for (int t = 0; t < kStreamT; ++t)  // (a negative edge compares as a huge unsigned one)
-            pass[t] &= whole_mask |
-                       __builtin_amdgcn_uicmp((uint32_t)(i0 + 32 * t), deg, 36 /*ULT*/);
-        }
-        // the few that pass go to the list as (draw, edge); the merge computes their exact keys
-        // (keeping the fixed-operation key out of this loop saves registers)
-        if (nb > kStreamBuf - kStreamChunk) flush();
-        const int hs = threadIdx.x & 32;
-#pragma unroll
-        for (int t = 0; t < kStreamT; ++t) {
-          if (pass[t] == 0) continue;
-          const uint32_t b = (uint32_t)(pass[t] >> hs);
-          if ((b >> l) & 1u) {
-            const int pos = nb + __builtin_popcount(b & ((1u << l) - 1u));
-            s_x[g][pos] = xs[t];
-            s_i[g][pos] = (uint32_t)(i0 + 32 * t);
-            s_h[g][pos] = (int32_t)h;
-          }
-          nb += __builtin_popcount(b);
-        }
-      }
     }
-    if (p0 >= p1) break;
-    uint32_t gr = 0;
-    if (l == 0) gr = (uint32_t)atomicAdd((unsigned long long *)(a.hub.count + 8 + px),
-                                         (unsigned long long)kBiasGrab);
-    c0 = p0 + (uint32_t)__shfl((int32_t)gr, 0, 32);
-    if (c0 >= p1) break;
-    c1 = c0 + kBiasGrab < p1 ? c0 + kBiasGrab : p1;
+    if (skip) continue;
+    const uint32_t q = ch - hstart;
+    const int32_t i0 = chunk_i0(q);
+    const bool whole = chunk_whole(i0);
+    if (!have_next) load_probs(q, pn);
+    float p[kStreamT];
+#pragma unroll
+    for (int t = 0; t < kStreamT; ++t) p[t] = pn[t];
+    have_next = ch + 1 < c1 && ch + 1 < hnext;
+    if (have_next) load_probs(q + 1, pn);
+    const uint32_t bc = (jb >> 2) + q * (kStreamT / 4);
+    uint32_t xs[kStreamT];
+#pragma unroll
+    for (int bq = 0; bq < kStreamT / 4; ++bq) {
+      const uint4 o = philox4x32_10(make_uint4(bc + bq, 0u, sub, 0u), kk);
+      xs[4 * bq + 0] = o.x;
+      xs[4 * bq + 1] = o.y;
+      xs[4 * bq + 2] = o.z;
+      xs[4 * bq + 3] = o.w;
+    }
+    // Per step t, the wave's lanes whose edge passes the cheap bound, straight from the compares
+    // (lin_pass_mask: one convert, one fma and one compare per edge; round 3 A/B against the
+    // hardware-log2 bound: +1.7 %); the valid-edge compare only matters in a row's first and
+    // last chunks.
+    uint64_t pass[kStreamT];
+#pragma unroll
+    for (int t = 0; t < kStreamT; ++t) pass[t] = lin_pass_mask(xs[t], p[t], cx);
+    const uint64_t whole_mask = __ballot(whole);
+    if (whole_mask != __builtin_amdgcn_read_exec()) {  // (wave-uniform: a row's first / last chunk)
+#pragma unroll
+      for (int t = 0; t < kStreamT; ++t)  // (a negative edge compares as a huge unsigned one)
+        pass[t] &= whole_mask | __builtin_amdgcn_uicmp((uint32_t)(i0 + 32 * t), deg, 36 /*ULT*/);
+    }
+    // the few that pass go to the list as (draw, edge); the merge computes their exact keys
+    // (keeping the fixed-operation key out of this loop saves registers)
+    if (nb > kStreamBuf - kStreamChunk) flush();
+    const int hs = threadIdx.x & 32;
+#pragma unroll
+    for (int t = 0; t < kStreamT; ++t) {
+      if (pass[t] == 0) continue;
+      const uint32_t b = (uint32_t)(pass[t] >> hs);
+      if ((b >> l) & 1u) {
+        const int pos = nb + __builtin_popcount(b & ((1u << l) - 1u));
+        s_x[g][pos] = xs[t];
+        s_i[g][pos] = (uint32_t)(i0 + 32 * t);
+        s_h[g][pos] = (int32_t)h;
+      }
+      nb += __builtin_popcount(b);
+    }
   }
   if (nb > 0) flush();
 }
 
 __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const int64_t *bsum,
                                                            int64_t *boff, int64_t *d_nnz,
-                                                           uint64_t *stamp, int dyn) {
+                                                           uint64_t *stamp) {
   // profiling only (DGS_PROF_HUB: stamp != nullptr, a kernel argument: uniform branch)
   if (stamp && threadIdx.x == 0) stamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-  bias_stream_body(a, bsum, boff, d_nnz, dyn);
+  bias_stream_body(a, bsum, boff, d_nnz);
   if (stamp) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1771,13 +1697,12 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   const bool bias_hubs = bias && !replace && k > 0 && S < kHubMaxRows;
   // Two hub counters used by alternate hops (a global hop serial, so calls chain correctly):
   // each prep zeroes the other one; zeroed once at allocation.
-  // Each group is 16 words: the packed count, then (words 8-15) the uniform hub kernel's pools.
-  if (ws.hubcount.ensure(256)) DGS_HIP(hipMemsetAsync(ws.hubcount.p, 0, 256, st));
+  if (ws.hubcount.ensure(128)) DGS_HIP(hipMemsetAsync(ws.hubcount.p, 0, 128, st));
   const uint64_t par = ws.hop_serial++ & 1;
   ws.hub.ensure(HubView::bytes(S));
   HubView hub = HubView::make(ws.hub.as<int64_t>(), S);
-  hub.count = ws.hubcount.as<int64_t>() + 16 * par;
-  int64_t *next_count = ws.hubcount.as<int64_t>() + 16 * (par ^ 1);
+  hub.count = ws.hubcount.as<int64_t>() + 8 * par;
+  int64_t *next_count = ws.hubcount.as<int64_t>() + 8 * (par ^ 1);
   const bool bias_replace = bias && replace;
   ws.tpre.ensure(sizeof(int32_t) * (size_t)(2 * S));
   int32_t *tpre = ws.tpre.as<int32_t>();
@@ -1848,8 +1773,7 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     const int64_t row_blocks = ceil_div(S, kRowsPerBlock);
     if (use_hubs) {
       hipLaunchKernelGGL(k_hub_reservoir, dim3(hub_blocks()), dim3(256), 0, st, ua,
-                         (const int64_t *)bsum, boff, d_nnz, profile_stamps(3, hub_blocks()),
-                         hub_dyn());
+                         (const int64_t *)bsum, boff, d_nnz, profile_stamps(3, hub_blocks()));
       DGS_LAUNCH_CHECK();
     }
     if (replace)
@@ -1894,7 +1818,7 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
       // (its workgroup 0 also does the hop's tile-offset scan)
       hipLaunchKernelGGL(k_bias_stream, dim3(bias_stream_blocks()), dim3(kTileRows), 0, st, ba,
                          (const int64_t *)bsum, boff, d_nnz,
-                         profile_stamps(4, bias_stream_blocks()), bias_dyn());
+                         profile_stamps(4, bias_stream_blocks()));
       DGS_LAUNCH_CHECK();
       if (stats) {  // candidates per hub row after the stream
         DGS_HIP(hipStreamSynchronize(st));
