@@ -433,7 +433,11 @@ def main():
     # every rank builds them in the same order)
     everything = hot if hot is not None else torch.arange(N)
     ref = None
-    if world > 1 and mode != "replicated":
+    # built only when something uses them (a graph that fits one GPU's HBM only when sharded
+    # runs with --no-replicated-pass --check-batches 0: the self-check then compares against
+    # this layout's own sequential loop, and the xGMI pass samples with this layout's sampler)
+    need_ref = not args.no_replicated_pass or args.check_batches > 0
+    if world > 1 and mode != "replicated" and need_ref:
         ref = (dgs.classes.P2PCacheSampler(indptr, indices, probs, everything, dev_index),
                dgs.classes.P2PCacheFeatureServer(feats, everything, dev_index))
     self_check = None

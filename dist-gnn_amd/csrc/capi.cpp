@@ -32,6 +32,14 @@ int guard(F &&f) {
 
 hipStream_t S(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
+// The object behind a handle; a null handle (or one whose object is gone) is an error, not a
+// crash (the Python binding passes None once an object has been destroyed).
+template <typename H>
+auto &obj(H *h, const char *what) {
+  if (!h || !h->s) throw Error(std::string(what) + ": null handle (destroyed?)");
+  return *h->s;
+}
+
 // Pointer usable by kernels: device memory or registered/pinned host memory.
 template <typename T>
 T *dev_ptr(T *p, const char *what) {
@@ -221,18 +229,42 @@ int dgs_host_unregister(void *ptr) {
   });
 }
 
-// ------------------------------------------------------------------ ops
-int dgs_index_select(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
-                     int64_t n, void *out, void *stream) {
+// ------------------------------------------------------------------ async errors, streams
+int dgs_check_async_errors(void) {
+  return guard([&] { check_async_errors(); });
+}
+
+int dgs_stream_create(int priority, void **out) {
   return guard([&] {
-    gather_plain(dev_ptr(data, "data"), row_bytes, dev_ptr(nid, "nid"), nid_bytes, n, out,
-                 S(stream));
+    hipStream_t st = nullptr;
+    DGS_HIP(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, priority));
+    *out = st;
   });
 }
 
-int dgs_index_select_device(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
-                            int64_t n, void *out, void *stream) {
-  return guard([&] { gather_plain(data, row_bytes, nid, nid_bytes, n, out, S(stream)); });
+int dgs_stream_destroy(void *stream) {
+  return guard([&] {
+    DGS_CHECK(stream, "stream_destroy: the null stream is not the library's");
+    DGS_HIP(hipStreamDestroy(S(stream)));
+  });
+}
+
+// ------------------------------------------------------------------ ops
+int dgs_index_select(const void *data, int64_t num_rows, int64_t row_bytes, const void *nid,
+                     int nid_bytes, int64_t n, void *out, void *stream) {
+  return guard([&] {
+    check_async_errors();
+    gather_plain(dev_ptr(data, "data"), num_rows, row_bytes, dev_ptr(nid, "nid"), nid_bytes, n,
+                 out, S(stream));
+  });
+}
+
+int dgs_index_select_device(const void *data, int64_t num_rows, int64_t row_bytes,
+                            const void *nid, int nid_bytes, int64_t n, void *out, void *stream) {
+  return guard([&] {
+    check_async_errors();
+    gather_plain(data, num_rows, row_bytes, nid, nid_bytes, n, out, S(stream));
+  });
 }
 
 int dgs_stream_wait(void *producer, void *consumer) {
@@ -248,17 +280,18 @@ int dgs_stream_wait_event(void *event, void *consumer) {
 
 int dgs_loader_gather(dgs_sampler *s, dgs_feature_server *fs, void *producer, void *consumer,
                       const int64_t *nids, int64_t n, void *feat_out, const void *labels,
-                      int64_t label_row_bytes, const int64_t *seeds, int64_t n_seeds,
-                      void *label_out) {
+                      int64_t label_rows, int64_t label_row_bytes, const int64_t *seeds,
+                      int64_t n_seeds, void *label_out) {
   return guard([&] {
+    check_async_errors();
     if (s)
-      s->s->wait_ended(S(producer), S(consumer));
+      obj(s, "sampler").wait_ended(S(producer), S(consumer));
     else
       stream_wait_impl(producer, consumer);
     const bool want_labels = labels && n_seeds > 0;
     // 4- and 8-byte label rows ride in the feature gather's launch
     // (a zero-width feature matrix launches no gather: its labels go on their own)
-    const bool fuse = want_labels && fs && n > 0 && fs->s->row_bytes() > 0 &&
+    const bool fuse = want_labels && fs && n > 0 && obj(fs, "feature server").row_bytes() > 0 &&
                       n_seeds < (int64_t(1) << 31) &&
                       (label_row_bytes == 4 || label_row_bytes == 8) &&
                       ((uintptr_t)labels % label_row_bytes) == 0 &&
@@ -268,12 +301,15 @@ int dgs_loader_gather(dgs_sampler *s, dgs_feature_server *fs, void *producer, vo
       lt.data = (const char *)labels;
       lt.ids = seeds;
       lt.out = (char *)label_out;
+      lt.nrows = (uint64_t)(label_rows > 0 ? label_rows : 0);
       lt.n = (uint32_t)n_seeds;
       lt.row_bytes = (uint32_t)label_row_bytes;
     }
-    if (fs && n > 0) fs->s->gather(nids, n, feat_out, S(consumer), fuse ? &lt : nullptr);
+    if (fs && n > 0) obj(fs, "feature server").gather(nids, n, feat_out, S(consumer),
+                                                      fuse ? &lt : nullptr);
     if (want_labels && !fuse)
-      gather_plain(labels, label_row_bytes, seeds, 8, n_seeds, label_out, S(consumer));
+      gather_plain(labels, label_rows, label_row_bytes, seeds, 8, n_seeds, label_out,
+                   S(consumer));
   });
 }
 
@@ -425,14 +461,15 @@ int dgs_p2p_server_create(const void *src, int64_t items, int64_t item_bytes,
 
 int dgs_p2p_server_device_ptr(dgs_p2p_server *s, int64_t rank, void **ptr, int64_t *items) {
   return guard([&] {
-    DGS_CHECK(rank >= 0 && rank < s->s->world(), "rank out of range");
-    *ptr = s->s->ptr((int)rank);
-    *items = s->s->items((int)rank);
+    DGS_CHECK(rank >= 0 && rank < obj(s, "p2p server").world(), "rank out of range");
+    *ptr = obj(s, "p2p server").ptr((int)rank);
+    *items = obj(s, "p2p server").items((int)rank);
   });
 }
 
 int dgs_p2p_server_destroy(dgs_p2p_server *s) {
   return guard([&] {
+    if (!s) return;
     delete s->s;
     delete s;
   });
@@ -450,7 +487,7 @@ int dgs_sampler_create(const int64_t *indptr, const int64_t *indices, const floa
 
 int dgs_sampler_bounds(const dgs_sampler *s, int64_t n_seeds, const int64_t *fan_out, int L,
                        int64_t *frontier_cap, int64_t *edge_cap) {
-  return guard([&] { s->s->bounds(n_seeds, fan_out, L, frontier_cap, edge_cap); });
+  return guard([&] { obj(s, "sampler").bounds(n_seeds, fan_out, L, frontier_cap, edge_cap); });
 }
 
 int dgs_sampler_sample(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
@@ -458,7 +495,7 @@ int dgs_sampler_sample(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
                        int64_t *const *rows, int64_t *const *cols, int64_t *sizes_out,
                        void *stream) {
   return guard([&] {
-    s->s->sample(dev_ptr(seeds, "seeds"), n_seeds, fan_out, L, replace != 0, frontiers, rows,
+    obj(s, "sampler").sample(dev_ptr(seeds, "seeds"), n_seeds, fan_out, L, replace != 0, frontiers, rows,
                  cols, sizes_out, S(stream));
   });
 }
@@ -470,7 +507,7 @@ int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_see
                              void *stream) {
   return guard([&] {
     DGS_CHECK((flags & ~DGS_SAMPLE_HOST_ASYNC) == 0, "sample_begin: unknown flags");
-    s->s->sample_begin(dev_ptr(seeds, "seeds"), n_seeds, fan_out, L, replace != 0, frontiers,
+    obj(s, "sampler").sample_begin(dev_ptr(seeds, "seeds"), n_seeds, fan_out, L, replace != 0, frontiers,
                        rows, cols, S(stream), launch_seeds, (flags & DGS_SAMPLE_HOST_ASYNC) != 0);
   });
 }
@@ -497,8 +534,8 @@ int dgs_sampler_sample_packed(dgs_sampler *s, const int64_t *seeds, int64_t n_se
     if (n_seeds > 0) check_device_cached(seeds, "seeds");
     check_device_cached(out, "out");
     int64_t *fr[64], *rows[64], *cols[64];
-    packed_ptrs(*s->s, n_seeds, fan_out, L, out, fr, rows, cols);
-    s->s->sample(seeds, n_seeds, fan_out, L, replace != 0, fr, rows, cols, sizes_out, S(stream));
+    packed_ptrs(obj(s, "sampler"), n_seeds, fan_out, L, out, fr, rows, cols);
+    obj(s, "sampler").sample(seeds, n_seeds, fan_out, L, replace != 0, fr, rows, cols, sizes_out, S(stream));
   });
 }
 
@@ -513,11 +550,15 @@ int dgs_sampler_sample_begin_after(dgs_sampler *s, void *wait_for, const int64_t
               "sample_begin: DGS_SAMPLE_WAIT and DGS_SAMPLE_WAIT_EVENT exclude each other");
     DGS_CHECK(!(flags & DGS_SAMPLE_WAIT_EVENT) || wait_for,
               "sample_begin: DGS_SAMPLE_WAIT_EVENT needs an event");
+    // a handle without a flag is refused rather than ignored: callers written against the
+    // round-3 header (wait when wait_for != NULL) would otherwise silently get no wait
+    DGS_CHECK(!wait_for || (flags & (DGS_SAMPLE_WAIT | DGS_SAMPLE_WAIT_EVENT)),
+              "sample_begin: wait_for given without DGS_SAMPLE_WAIT or DGS_SAMPLE_WAIT_EVENT");
     DGS_CHECK(L > 0 && L <= 64, "sample_begin: 1 to 64 hops");
     if (n_seeds > 0) check_device_cached(seeds, "seeds");
     check_device_cached(out, "out");
     int64_t *fr[64], *rows[64], *cols[64];
-    packed_ptrs(*s->s, n_seeds, fan_out, L, out, fr, rows, cols);
+    packed_ptrs(obj(s, "sampler"), n_seeds, fan_out, L, out, fr, rows, cols);
     // DGS_SAMPLE_WAIT, not the handle, says whether to wait: NULL is the null stream (torch's
     // default current stream), a producer like any other.  (Rounds 2-3 tested the handle, so a
     // caller on the default stream got no wait at all -- round 4's root cause of the N = 2
@@ -526,42 +567,43 @@ int dgs_sampler_sample_begin_after(dgs_sampler *s, void *wait_for, const int64_t
     // or on an event the caller recorded earlier (where its seeds were complete)
     if (flags & DGS_SAMPLE_WAIT_EVENT)
       DGS_HIP(hipStreamWaitEvent(S(stream), reinterpret_cast<hipEvent_t>(wait_for), 0));
-    s->s->sample_begin(seeds, n_seeds, fan_out, L, replace != 0, fr, rows, cols, S(stream),
+    obj(s, "sampler").sample_begin(seeds, n_seeds, fan_out, L, replace != 0, fr, rows, cols, S(stream),
                        launch_seeds, (flags & DGS_SAMPLE_HOST_ASYNC) != 0);
   });
 }
 
 int dgs_sampler_sample_end(dgs_sampler *s, int L, int64_t *sizes_out, void *stream) {
-  return guard([&] { s->s->sample_end(L, sizes_out, S(stream)); });
+  return guard([&] { obj(s, "sampler").sample_end(L, sizes_out, S(stream)); });
 }
 
 int dgs_sampler_context_count(dgs_sampler *s, int64_t *n) {
-  return guard([&] { *n = (int64_t)s->s->num_contexts(); });
+  return guard([&] { *n = (int64_t)obj(s, "sampler").num_contexts(); });
 }
 
 int dgs_sampler_local_cache(const dgs_sampler *s, const int64_t **sub_indptr, int64_t *n_rows,
                             const int64_t **sub_indices, int64_t *n_edges,
                             const float **sub_probs) {
   return guard([&] {
-    *sub_indptr = s->s->sub_indptr();
-    *n_rows = s->s->n_rows();
-    *sub_indices = s->s->sub_indices();
-    *n_edges = s->s->n_edges();
-    *sub_probs = s->s->sub_probs();
+    *sub_indptr = obj(s, "sampler").sub_indptr();
+    *n_rows = obj(s, "sampler").n_rows();
+    *sub_indices = obj(s, "sampler").sub_indices();
+    *n_edges = obj(s, "sampler").n_edges();
+    *sub_probs = obj(s, "sampler").sub_probs();
   });
 }
 
 int dgs_sampler_cache_map_size(const dgs_sampler *s, int64_t *n) {
-  return guard([&] { *n = s->s->cache_map_size(); });
+  return guard([&] { *n = obj(s, "sampler").cache_map_size(); });
 }
 
 int dgs_sampler_cache_map_fill(const dgs_sampler *s, int64_t *key, int64_t *idx,
                                int64_t *devid, void *stream) {
-  return guard([&] { s->s->cache_map_fill(key, idx, devid, S(stream)); });
+  return guard([&] { obj(s, "sampler").cache_map_fill(key, idx, devid, S(stream)); });
 }
 
 int dgs_sampler_destroy(dgs_sampler *s) {
   return guard([&] {
+    if (!s) return;
     delete s->s;
     delete s;
   });
@@ -579,23 +621,27 @@ int dgs_feature_server_create(const void *data, int64_t num_rows, int64_t row_by
 
 int dgs_feature_server_gather(dgs_feature_server *s, const int64_t *nids, int64_t n, void *out,
                               void *stream) {
-  return guard([&] { s->s->gather(dev_ptr(nids, "nids"), n, out, S(stream)); });
+  return guard([&] {
+    check_async_errors();
+    obj(s, "feature server").gather(dev_ptr(nids, "nids"), n, out, S(stream));
+  });
 }
 
 int dgs_feature_server_local_cache(const dgs_feature_server *s, const void **ptr,
                                    int64_t *rows) {
   return guard([&] {
-    *ptr = s->s->local();
-    *rows = s->s->local_rows();
+    *ptr = obj(s, "feature server").local();
+    *rows = obj(s, "feature server").local_rows();
   });
 }
 
 int dgs_feature_server_layout(const dgs_feature_server *s, int *wshift) {
-  return guard([&] { *wshift = s->s->layout(); });
+  return guard([&] { *wshift = obj(s, "feature server").layout(); });
 }
 
 int dgs_feature_server_destroy(dgs_feature_server *s) {
   return guard([&] {
+    if (!s) return;
     delete s->s;
     delete s;
   });

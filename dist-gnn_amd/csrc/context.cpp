@@ -2,6 +2,7 @@
 #include "context.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -256,6 +257,50 @@ void *device_view(const void *p, int64_t bytes, bool *registered_here) {
   host_regs()[(uintptr_t)p] = HostReg{nb, 1};
   if (registered_here) *registered_here = true;
   return d;
+}
+
+// ------------------------------------------------------------------ async errors
+namespace {
+struct AsyncErrWords {
+  int64_t *host = nullptr, *dev = nullptr;
+  std::atomic<uint64_t> tag{0};
+};
+AsyncErrWords &async_err() {
+  static AsyncErrWords w;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void *h = nullptr;
+    // portable: visible to every device of the process; coherent: a kernel's system-scope
+    // store is seen by the host without a synchronisation
+    DGS_HIP(hipHostMalloc(&h, sizeof(int64_t) * kAsyncErrWords,
+                          hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+    std::memset(h, 0, sizeof(int64_t) * kAsyncErrWords);
+    void *d = nullptr;
+    DGS_HIP(hipHostGetDevicePointer(&d, h, 0));
+    w.host = static_cast<int64_t *>(h);
+    w.dev = static_cast<int64_t *>(d);
+  });
+  return w;
+}
+}  // namespace
+
+int64_t *async_err_dev() { return async_err().dev; }
+
+uint64_t async_err_next_tag() { return async_err().tag.fetch_add(1) + 1; }
+
+void check_async_errors() {
+  AsyncErrWords &w = async_err();
+  const int64_t kind = __atomic_load_n(&w.host[0], __ATOMIC_ACQUIRE);
+  if (kind == 0) return;
+  const int64_t id = w.host[1], rows = w.host[2], tag = w.host[3];
+  __atomic_store_n(&w.host[0], 0, __ATOMIC_RELEASE);
+  const char *what = kind == kAsyncErrFeature ? "feature gather (nids)"
+                     : kind == kAsyncErrLabel ? "label gather (seeds)"
+                                              : "index_select (nid)";
+  throw Error("an earlier " + std::string(what) + " call read id " + std::to_string(id) +
+              ", outside [0, " + std::to_string(rows) + "); its rows were filled from row 0 " +
+              "(gather call #" + std::to_string(tag) + " of this process; the reference reads " +
+              "out of bounds here)");
 }
 
 // ------------------------------------------------------------------ profiler

@@ -92,4 +92,16 @@ void host_pin(void *p, int64_t bytes);
 void host_unpin(void *p);
 bool is_device_pointer(const void *p);
 
+// Out-of-range ids met by the gather kernels (feature server, index_select, the loader's fused
+// label rows; the reference reads out of bounds there, feature_ops.cu:38-73,140-171).  The
+// kernel reads row 0 in place of the bad row and stores {kind, id, num_rows, tag} into these
+// coherent pinned host words with system-scope vector stores; no launch or synchronisation is
+// added.  The next gather entry point on the host (or dgs_check_async_errors) raises and clears
+// them.  kind: kAsyncErrFeature / kAsyncErrLabel / kAsyncErrSelect.
+constexpr int64_t kAsyncErrFeature = 1, kAsyncErrLabel = 2, kAsyncErrSelect = 3;
+constexpr int kAsyncErrWords = 4;
+int64_t *async_err_dev();  // device-visible address of the words (allocated on first use)
+uint64_t async_err_next_tag();  // per-process call counter (the tag a launch reports)
+void check_async_errors();     // throws (and clears) when a kernel stored an error
+
 }  // namespace dgs

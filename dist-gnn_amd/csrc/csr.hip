@@ -51,10 +51,13 @@ __global__ void k_ntab_init_host(NodeEntry *ntab, const int64_t *indptr, int64_t
   }
 }
 
-__global__ void k_ntab_assign(NodeEntry *ntab, const int64_t *nids, const int64_t *sub_indptr,
-                              int64_t n, int64_t loc, const int64_t *sub_indices) {
+// (the sampler range-checks its cache lists before this runs; the guard keeps a list that
+// slipped through from writing outside the table)
+__global__ void k_ntab_assign(NodeEntry *ntab, int64_t num_nodes, const int64_t *nids,
+                              const int64_t *sub_indptr, int64_t n, int64_t loc,
+                              const int64_t *sub_indices) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
+  if (i < n && (uint64_t)nids[i] < (uint64_t)num_nodes) {
     const int64_t b = sub_indptr[i], e = sub_indptr[i + 1];
     NodeEntry ne;
     ne.ptr = sub_indices + b;
@@ -143,9 +146,10 @@ __global__ void k_loctab_init(int64_t *tab, int64_t n) {
   if (i < n) tab[i] = ((int64_t)kLocHost << kLocShift) | i;
 }
 
-__global__ void k_loctab_assign(int64_t *tab, const int64_t *nids, int64_t n, int64_t loc) {
+__global__ void k_loctab_assign(int64_t *tab, int64_t num_nodes, const int64_t *nids, int64_t n,
+                                int64_t loc) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) tab[nids[i]] = (loc << kLocShift) | i;
+  if (i < n && (uint64_t)nids[i] < (uint64_t)num_nodes) tab[nids[i]] = (loc << kLocShift) | i;
 }
 
 __global__ void k_take_i64(const int64_t *src, const int64_t *idx, int64_t n, int64_t *out) {
@@ -204,11 +208,12 @@ void ntab_init_host(NodeEntry *ntab, const int64_t *indptr, int64_t n, const int
   DGS_LAUNCH_CHECK();
 }
 
-void ntab_assign(NodeEntry *ntab, const int64_t *nids, const int64_t *sub_indptr, int64_t n,
-                 int loc, const int64_t *sub_indices, hipStream_t st) {
+void ntab_assign(NodeEntry *ntab, int64_t num_nodes, const int64_t *nids,
+                 const int64_t *sub_indptr, int64_t n, int loc, const int64_t *sub_indices,
+                 hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_ntab_assign, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ntab,
-                     nids, sub_indptr, n, (int64_t)loc, sub_indices);
+                     num_nodes, nids, sub_indptr, n, (int64_t)loc, sub_indices);
   DGS_LAUNCH_CHECK();
 }
 
@@ -271,10 +276,11 @@ void loctab_init_host(int64_t *tab, int64_t n, hipStream_t st) {
   DGS_LAUNCH_CHECK();
 }
 
-void loctab_assign(int64_t *tab, const int64_t *nids, int64_t n, int loc, hipStream_t st) {
+void loctab_assign(int64_t *tab, int64_t num_nodes, const int64_t *nids, int64_t n, int loc,
+                   hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_loctab_assign, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, tab,
-                     nids, n, (int64_t)loc);
+                     num_nodes, nids, n, (int64_t)loc);
   DGS_LAUNCH_CHECK();
 }
 

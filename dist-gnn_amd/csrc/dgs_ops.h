@@ -16,22 +16,33 @@ struct LabelTail {
   const char *data = nullptr;
   const int64_t *ids = nullptr;
   char *out = nullptr;
+  uint64_t nrows = 0;  // rows of `data` (ids are range-checked against it)
   uint32_t n = 0;
   uint32_t row_bytes = 0;  // 4 or 8
   uint32_t blk0 = 0xffffffffu;  // first label workgroup (set by the launcher)
 };
+// Range guard of one gather launch (a kernel argument): ids outside [0, nrows) read row 0 and
+// are reported through the async error words (context.h) under `tag`, as error `kind`.
+struct GatherGuard {
+  uint64_t nrows = 0;
+  int64_t *err = nullptr;
+  int64_t tag = 0;
+  int64_t kind = 0;
+};
+// Every gather below checks its ids against the source's row count (nrows > 0 is required when
+// n > 0): an id outside [0, nrows) reads row 0 and the next gather entry point raises.
 // out[i, :] = data[nid[i], :], a row_bytes byte copy per row.
-void gather_plain(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
-                  int64_t n, void *out, hipStream_t st);
+void gather_plain(const void *data, int64_t nrows, int64_t row_bytes, const void *nid,
+                  int nid_bytes, int64_t n, void *out, hipStream_t st);
 // out[i, :] = *(row_bytes at ftab[nids[i]]): ftab holds the absolute (device-accessible)
 // address of every node's feature row.  align_or = OR of all row base addresses.
-void gather_table(const int64_t *ftab, uintptr_t align_or, int64_t row_bytes,
+void gather_table(const int64_t *ftab, int64_t nrows, uintptr_t align_or, int64_t row_bytes,
                   const int64_t *nids, int64_t n, void *out, hipStream_t st,
-                    const LabelTail *tail = nullptr);
+                  const LabelTail *tail = nullptr);
 // Strided cache layout (every node cached, node v at row v >> wshift of GPU v & (W - 1),
 // W = 1 << wshift <= 8; W = 1 is the whole-graph-in-HBM identity layout): the row address is
 // computed, so the gather reads no per-node table.  bases[d] = GPU d's (IPC-mapped) block.
-void gather_strided(const void *const *bases, int wshift, int64_t row_bytes,
+void gather_strided(const void *const *bases, int wshift, int64_t nrows, int64_t row_bytes,
                     const int64_t *nids, int64_t n, void *out, hipStream_t st,
                     const LabelTail *tail = nullptr);
 // number of i < n with list[i] != start + i * stride (device count -> host)
@@ -39,9 +50,11 @@ int64_t count_stride_mismatch(const int64_t *list, int64_t n, int64_t start, int
                               hipStream_t st);
 // ftab[v] = base + v * row_bytes for v < n
 void ftab_init(int64_t *ftab, int64_t n, const void *base, int64_t row_bytes, hipStream_t st);
-// ftab[nids[i]] = base + i * row_bytes
-void ftab_assign(int64_t *ftab, const int64_t *nids, int64_t n, const void *base,
-                 int64_t row_bytes, hipStream_t st);
+// number of i < n with list[i] outside [0, num_rows) (device count -> host)
+int64_t count_out_of_range(const int64_t *list, int64_t n, int64_t num_rows, hipStream_t st);
+// ftab[nids[i]] = base + i * row_bytes (ids outside [0, num_rows) are skipped)
+void ftab_assign(int64_t *ftab, int64_t num_rows, const int64_t *nids, int64_t n,
+                 const void *base, int64_t row_bytes, hipStream_t st);
 
 // ---------------------------------------------------------------- CSR utilities (csr.hip)
 // sub_indptr[i] = sum_{j<i} deg(nids[j]), i = 0..n
@@ -54,8 +67,10 @@ void extract_edge_data(const int64_t *nids, int64_t n, const int64_t *indptr,
 void ntab_init_host(NodeEntry *ntab, const int64_t *indptr, int64_t n, const int64_t *indices,
                     hipStream_t st);
 // ntab[nids[i]] = {sub_indices + sub_indptr[i], (sub_indptr[i+1]-sub_indptr[i]) | loc << 56}
-void ntab_assign(NodeEntry *ntab, const int64_t *nids, const int64_t *sub_indptr, int64_t n,
-                 int loc, const int64_t *sub_indices, hipStream_t st);
+// (ids outside [0, num_nodes) are skipped)
+void ntab_assign(NodeEntry *ntab, int64_t num_nodes, const int64_t *nids,
+                 const int64_t *sub_indptr, int64_t n, int loc, const int64_t *sub_indices,
+                 hipStream_t st);
 // Compacts a (loc << 56 | row) table into (nid, row, loc) triples for every node whose
 // location is a GPU; *d_count receives the count.  key/idx/devid may be null (count only).
 void cache_map_compact(const int64_t *tab, int64_t n, int64_t *key, int64_t *idx,
@@ -179,6 +194,7 @@ void profile_collect();
 void profile_reserve();
 // cache-map helpers: tab[v] = (loc << 56) | row
 void loctab_init_host(int64_t *tab, int64_t n, hipStream_t st);
-void loctab_assign(int64_t *tab, const int64_t *nids, int64_t n, int loc, hipStream_t st);
+void loctab_assign(int64_t *tab, int64_t num_nodes, const int64_t *nids, int64_t n, int loc,
+                   hipStream_t st);
 
 }  // namespace dgs

@@ -14,6 +14,7 @@
 // table load per row (TableSrc) instead of a hash probe chain plus a second pass.
 #include <hip/hip_ext.h>
 
+#include "context.h"
 #include "dgs_common.h"
 #include "dgs_ops.h"
 
@@ -148,11 +149,22 @@ struct StridedSrc {
 constexpr int kGatherThreads = DGS_GATHER_THREADS;
 constexpr int kGatherUnroll = DGS_GATHER_UNROLL;
 
+// Stores the first out-of-range id a launch met into the process's async error words
+// (context.h): id, row count and call tag first, then the kind with a system-scope release.
+__device__ __attribute__((noinline)) void report_bad_id(int64_t *err, int64_t kind, int64_t id,
+                                                        uint64_t rows, int64_t tag) {
+  __hip_atomic_store(err + 1, id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(err + 2, (int64_t)rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(err + 3, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(err, kind, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <int V, typename Src>
 __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nchunks,
                                                            uint32_t cpr, FastDivU32 fd,
                                                            char *__restrict__ out,
-                                                           uint64_t *stamp, LabelTail lt) {
+                                                           uint64_t *stamp, LabelTail lt,
+                                                           GatherGuard gd) {
   using T = typename VecT<V>::T;
 #if DGS_GATHER_PRIO
   // issue priority over co-resident waves of other kernels (the sampler's VALU-bound waves
@@ -162,13 +174,17 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nch
   if (blockIdx.x >= lt.blk0) {  // fused label rows (uniform branch), one per lane
     const uint32_t i = (blockIdx.x - lt.blk0) * (uint32_t)kGatherThreads + threadIdx.x;
     if (i < lt.n) {
-      const int64_t id = lt.ids[i];
+      const int64_t raw = lt.ids[i];
+      // range guard: an id outside [0, label rows) reads row 0 and is reported
+      const bool bad = (uint64_t)raw >= lt.nrows;
+      const int64_t id = bad ? 0 : raw;
       if (lt.row_bytes == 8)
         reinterpret_cast<uint64_t *>(lt.out)[i] =
             *to_global<uint64_t>(lt.data + (size_t)id * 8);
       else
         reinterpret_cast<uint32_t *>(lt.out)[i] =
             *to_global<uint32_t>(lt.data + (size_t)id * 4);
+      if (bad) report_bad_id(gd.err, kAsyncErrLabel, raw, lt.nrows, gd.tag);
     }
     return;
   }
@@ -190,6 +206,17 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nch
   }
 #pragma unroll
   for (int u = 0; u < kGatherUnroll; ++u) key[u] = src.key(r[u]);
+  // Range guard (one unsigned compare per id): an id outside [0, nrows) would address memory
+  // outside the source (a GPU fault); it reads row 0 instead and the launch reports it.
+  bool bad = false;
+  int64_t bad_id = 0;
+#pragma unroll
+  for (int u = 0; u < kGatherUnroll; ++u) {
+    const bool b = (uint64_t)key[u] >= gd.nrows;
+    bad_id = b ? (int64_t)key[u] : bad_id;
+    bad |= b;
+    key[u] = b ? 0 : key[u];
+  }
 #pragma unroll
   for (int u = 0; u < kGatherUnroll; ++u) a[u] = src.addr(key[u]);
 #pragma unroll
@@ -204,6 +231,7 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nch
     // streams past L2 instead of evicting the rows other waves are fetching
     if (g < nchunks) __builtin_nontemporal_store(v[u], reinterpret_cast<T *>(out + (size_t)g * V));
   }
+  if (bad) report_bad_id(gd.err, gd.kind, bad_id, gd.nrows, gd.tag);
   if (stamp) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have landed
     __syncthreads();
@@ -213,7 +241,7 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nch
 
 template <typename Src>
 void launch_gather_v(int V, Src src, int64_t n, int64_t row_bytes, char *out, hipStream_t st,
-                     int which, const LabelTail *tail = nullptr) {
+                     int which, GatherGuard gd, const LabelTail *tail = nullptr) {
   const int64_t cpr = row_bytes / V;
   DGS_CHECK(cpr > 0 && cpr < (int64_t(1) << 30), "gather: unsupported row size");
   const int64_t max_rows = ((int64_t(1) << 31) - kGatherThreads * kGatherUnroll) / cpr;
@@ -236,11 +264,11 @@ void launch_gather_v(int V, Src src, int64_t n, int64_t row_bytes, char *out, hi
     const dim3 block(kGatherThreads);
     const uint32_t c32 = (uint32_t)cpr;
     switch (V) {
-      case 16: hipLaunchKernelGGL((k_gather<16, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt); break;
-      case 8: hipLaunchKernelGGL((k_gather<8, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt); break;
-      case 4: hipLaunchKernelGGL((k_gather<4, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt); break;
-      case 2: hipLaunchKernelGGL((k_gather<2, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt); break;
-      default: hipLaunchKernelGGL((k_gather<1, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt); break;
+      case 16: hipLaunchKernelGGL((k_gather<16, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
+      case 8: hipLaunchKernelGGL((k_gather<8, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
+      case 4: hipLaunchKernelGGL((k_gather<4, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
+      case 2: hipLaunchKernelGGL((k_gather<2, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
+      default: hipLaunchKernelGGL((k_gather<1, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
     }
     DGS_LAUNCH_CHECK();
   }
@@ -257,42 +285,67 @@ __global__ void k_ftab_init(int64_t *ftab, int64_t n, const char *base, int64_t 
   if (i < n) ftab[i] = (int64_t)(base + i * row_bytes);
 }
 
-__global__ void k_ftab_assign(int64_t *ftab, const int64_t *nids, int64_t n, const char *base,
-                              int64_t row_bytes) {
+// (cache lists are range-checked by the services before this runs; the guard keeps a list
+// that slipped through from writing outside the table)
+__global__ void k_ftab_assign(int64_t *ftab, int64_t num_rows, const int64_t *nids, int64_t n,
+                              const char *base, int64_t row_bytes) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) ftab[nids[i]] = (int64_t)(base + i * row_bytes);
+  if (i < n) {
+    const int64_t v = nids[i];
+    if ((uint64_t)v < (uint64_t)num_rows) ftab[v] = (int64_t)(base + i * row_bytes);
+  }
 }
 
 }  // namespace
 
-void gather_plain(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
-                  int64_t n, void *out, hipStream_t st) {
+// Guard of one gather call: ids are checked against nrows (kind says which op reports).
+static GatherGuard make_guard(int64_t nrows, int64_t kind) {
+  DGS_CHECK(nrows > 0, "gather: ids into a source with no rows (every id is out of range)");
+  GatherGuard gd;
+  gd.nrows = (uint64_t)nrows;
+  gd.err = async_err_dev();
+  gd.tag = (int64_t)async_err_next_tag();
+  gd.kind = kind;
+  return gd;
+}
+
+static const LabelTail *checked_tail(const LabelTail *tail) {
+  if (tail && tail->n > 0)
+    DGS_CHECK(tail->nrows > 0, "label gather: seeds into a label array with no rows");
+  return tail;
+}
+
+void gather_plain(const void *data, int64_t nrows, int64_t row_bytes, const void *nid,
+                  int nid_bytes, int64_t n, void *out, hipStream_t st) {
   if (n <= 0 || row_bytes <= 0) return;
+  const GatherGuard gd = make_guard(nrows, kAsyncErrSelect);
   const int V = pick_vec(row_bytes, (uintptr_t)data | (uintptr_t)out);
   if (nid_bytes == 8) {
     PlainSrc<int64_t> s{(const char *)data, (const int64_t *)nid, row_bytes, 0};
-    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 2);
+    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 2, gd);
   } else {
     DGS_CHECK(nid_bytes == 4, "index ids must be int32 or int64");
     PlainSrc<int32_t> s{(const char *)data, (const int32_t *)nid, row_bytes, 0};
-    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 2);
+    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 2, gd);
   }
 }
 
-void gather_table(const int64_t *ftab, uintptr_t align_or, int64_t row_bytes,
+void gather_table(const int64_t *ftab, int64_t nrows, uintptr_t align_or, int64_t row_bytes,
                   const int64_t *nids, int64_t n, void *out, hipStream_t st,
                   const LabelTail *tail) {
   if (n <= 0 || row_bytes <= 0) return;
+  const GatherGuard gd = make_guard(nrows, kAsyncErrFeature);
   const int V = pick_vec(row_bytes, align_or | (uintptr_t)out);
   TableSrc s{ftab, nids, row_bytes, 0};
-  launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0, tail);
+  launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0, gd, checked_tail(tail));
 }
 
-void gather_strided(const void *const *bases, int wshift, int64_t row_bytes,
+void gather_strided(const void *const *bases, int wshift, int64_t nrows, int64_t row_bytes,
                     const int64_t *nids, int64_t n, void *out, hipStream_t st,
                     const LabelTail *tail) {
   if (n <= 0 || row_bytes <= 0) return;
   DGS_CHECK(wshift >= 0 && wshift <= 3, "strided gather: at most 8 locations");
+  const GatherGuard gd = make_guard(nrows, kAsyncErrFeature);
   const int W = 1 << wshift;
   const char *b[8];
   uintptr_t align_or = (uintptr_t)out;
@@ -303,11 +356,11 @@ void gather_strided(const void *const *bases, int wshift, int64_t row_bytes,
   const int V = pick_vec(row_bytes, align_or);
   if (wshift == 0) {
     StridedSrc<false> s{nids, b[0], b[1], b[2], b[3], b[4], b[5], b[6], b[7], row_bytes, 0, 0};
-    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0, tail);
+    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0, gd, checked_tail(tail));
   } else {
     StridedSrc<true> s{nids, b[0], b[1], b[2], b[3], b[4], b[5], b[6], b[7], row_bytes, 0,
                        (uint32_t)wshift};
-    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0, tail);
+    launch_gather_v(V, s, n, row_bytes, (char *)out, st, 0, gd, checked_tail(tail));
   }
 }
 
@@ -319,21 +372,40 @@ __global__ void k_stride_mismatch(const int64_t *list, int64_t n, int64_t start,
   const unsigned long long c = __popcll(__ballot(miss));
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(bad, c);
 }
-}  // namespace
 
-int64_t count_stride_mismatch(const int64_t *list, int64_t n, int64_t start, int64_t stride,
-                              hipStream_t st) {
+__global__ void k_out_of_range(const int64_t *list, int64_t n, int64_t num_rows,
+                               unsigned long long *bad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool miss = i < n && (uint64_t)list[i] >= (uint64_t)num_rows;
+  const unsigned long long c = __popcll(__ballot(miss));
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(bad, c);
+}
+
+template <typename K, typename... A>
+int64_t count_on_device(K kernel, int64_t n, hipStream_t st, A... args) {
   if (n <= 0) return 0;
   unsigned long long *bad = nullptr, h = 0;
   DGS_HIP(hipMalloc(&bad, sizeof(*bad)));
   DGS_HIP(hipMemsetAsync(bad, 0, sizeof(*bad), st));
-  hipLaunchKernelGGL(k_stride_mismatch, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, list,
-                     n, start, stride, bad);
-  DGS_LAUNCH_CHECK();
-  DGS_HIP(hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, st));
-  DGS_HIP(hipStreamSynchronize(st));
-  DGS_HIP(hipFree(bad));
+  hipLaunchKernelGGL(kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, args..., bad);
+  const hipError_t le = hipGetLastError();
+  if (le == hipSuccess) {
+    (void)hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+  }
+  (void)hipFree(bad);
+  DGS_HIP(le);
   return (int64_t)h;
+}
+}  // namespace
+
+int64_t count_stride_mismatch(const int64_t *list, int64_t n, int64_t start, int64_t stride,
+                              hipStream_t st) {
+  return count_on_device(k_stride_mismatch, n, st, list, n, start, stride);
+}
+
+int64_t count_out_of_range(const int64_t *list, int64_t n, int64_t num_rows, hipStream_t st) {
+  return count_on_device(k_out_of_range, n, st, list, n, num_rows);
 }
 
 void ftab_init(int64_t *ftab, int64_t n, const void *base, int64_t row_bytes, hipStream_t st) {
@@ -343,11 +415,11 @@ void ftab_init(int64_t *ftab, int64_t n, const void *base, int64_t row_bytes, hi
   DGS_LAUNCH_CHECK();
 }
 
-void ftab_assign(int64_t *ftab, const int64_t *nids, int64_t n, const void *base,
-                 int64_t row_bytes, hipStream_t st) {
+void ftab_assign(int64_t *ftab, int64_t num_rows, const int64_t *nids, int64_t n,
+                 const void *base, int64_t row_bytes, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_ftab_assign, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ftab,
-                     nids, n, (const char *)base, row_bytes);
+                     num_rows, nids, n, (const char *)base, row_bytes);
   DGS_LAUNCH_CHECK();
 }
 

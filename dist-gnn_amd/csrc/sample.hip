@@ -1411,8 +1411,13 @@ __device__ __forceinline__ void bias_stream_body(const BiasHubArgs &a, const int
   __shared__ int32_t s_h[kTileRows / 32][kStreamBuf];
   const int g = threadIdx.x >> 5;
   int nb = 0;  // entries in the list (half-wave uniform)
+  // The flush reads entries other lanes of the half-wave wrote: wavefront-scope fences around
+  // the scheduling barriers order those LDS accesses (a wave barrier alone only keeps the
+  // compiler from moving code across it).
   auto flush = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (int e0 = 0; e0 < nb; e0 += 32) {
       const int e = e0 + l;
       const bool v = e < nb;
@@ -1438,7 +1443,9 @@ __device__ __forceinline__ void bias_stream_body(const BiasHubArgs &a, const int
         todo &= ~same;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     nb = 0;
   };
   load_row(h);
@@ -1714,12 +1721,18 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   const int64_t nworkers = (int64_t)bias_stream_blocks() * (kTileRows / 32);
   BiasCand cand{};
   if (bias_hubs) {
-    // Hub rows have degree > kBiasHubT and are distinct within a hop: at most
-    // min(S, E / kBiasHubT) of them, with at most E / kStreamChunk + 2 per hub chunks.  The room is
-    // capped by a budget (DGS_BIAS_CAND_BUDGET entries, default 2^26 = 512 MB per context):
-    // rows past it get no room and are recomputed exactly (rare; correct either way).
-    const int64_t hubs_ub =
-        src.num_edges > 0 ? std::min<int64_t>(S, src.num_edges / kBiasHubT + 1) : S;
+    // Hub rows have degree > kBiasHubT.  After the first hop the seeds are a frontier (unique
+    // ids, and the sampler passes the previous hop's relabel tail): at most min(S, E / kBiasHubT)
+    // hub rows, with at most E / kStreamChunk + 2 per hub chunks.  The first hop's seeds (and the
+    // standalone op's) may repeat, so a hub row may count several times: the row bound is S
+    // there, and repeated rows' chunks may run past the chunk bound.  Rows whose room lies past
+    // the limit get none and are recomputed exactly by the merge (correct either way; only
+    // slower).  The room is also capped by a budget (DGS_BIAS_CAND_BUDGET entries, default
+    // 2^26 = 512 MB per context).
+    const bool seeds_unique = tail != nullptr;
+    const int64_t hubs_ub = src.num_edges > 0 && seeds_unique
+                                ? std::min<int64_t>(S, src.num_edges / kBiasHubT + 1)
+                                : S;
     const int64_t chunks =
         src.num_edges > 0 ? src.num_edges / kStreamChunk + 2 * hubs_ub : (int64_t(1) << 22);
     static const int64_t budget = [] {

@@ -61,6 +61,9 @@ void P2PServer::share() {
 }
 
 P2PServer::~P2PServer() {
+  // views of the block (and of the peers' blocks) may still be read by work queued on any
+  // stream of this device: it finishes before the mappings go
+  (void)hipDeviceSynchronize();
   try {
     if (world_ > 1)
       for (int i = 0; i < world_; ++i)
@@ -121,8 +124,13 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
   if (bias_) h_probs_.attach(probs, num_edges * 4);
   const int64_t *d_indptr = (const int64_t *)h_indptr_.dev;
 
-  // this rank's cached sub-CSR (sampler.cc:89-110)
+  // this rank's cached sub-CSR (sampler.cc:89-110).  A cached id outside [0, num_nodes) is
+  // refused here (the reference reads indptr out of bounds, utils.cu:12-42).
   int64_t *nids = device_copy_ids(cache_nids, n_cache, st);
+  if (count_out_of_range(nids, n_cache, num_nodes, st) != 0) {
+    (void)hipFree(nids);
+    DGS_CHECK(false, "cache_nids: an id is outside [0, num_nodes)");
+  }
   int64_t *sub_indptr = nullptr;
   DGS_HIP(hipMalloc(&sub_indptr, sizeof(int64_t) * (size_t)(n_cache + 1)));
   extract_indptr(nids, n_cache, d_indptr, sub_indptr, st);
@@ -148,8 +156,9 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
   NodeEntry *ntab = ntab_.as<NodeEntry>();
   ntab_init_host(ntab, d_indptr, num_nodes, (const int64_t *)h_indices_.dev, st);
   for (int d : rotation(rank_, world_))
-    ntab_assign(ntab, (const int64_t *)nids_srv_->ptr(d), (const int64_t *)indptr_srv_->ptr(d),
-                nids_srv_->items(d), d, (const int64_t *)indices_srv_->ptr(d), st);
+    ntab_assign(ntab, num_nodes, (const int64_t *)nids_srv_->ptr(d),
+                (const int64_t *)indptr_srv_->ptr(d), nids_srv_->items(d), d,
+                (const int64_t *)indices_srv_->ptr(d), st);
   DGS_HIP(hipStreamSynchronize(st));
 
   src_.ntab = ntab;
@@ -170,7 +179,10 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
 }
 
 // Stops a context's launcher thread and waits for its last call's kernels (the last relabel pass
-// may still run) before its buffers go.
+// may still run) before its buffers go.  A job the launcher thread has taken is launched to the
+// end (join waits for it) and its end event waited on; a job it has not taken is dropped
+// unlaunched.  launch() records the end event also when it fails part way, so the event
+// always follows every kernel the context enqueued.
 void Sampler::retire(Ctx &c) {
   if (c.launcher.joinable()) {
     {
@@ -194,6 +206,9 @@ void Sampler::retire(Ctx &c) {
 Sampler::~Sampler() {
   for (auto &kv : ctxs_) retire(*kv.second);
   ctxs_.clear();
+  // the graph's device copies may still be read by a call whose context was already retired
+  // by a failing caller: nothing of this device runs when they go
+  (void)hipDeviceSynchronize();
   delete indptr_srv_;
   delete indices_srv_;
   delete probs_srv_;
@@ -381,8 +396,23 @@ void Sampler::launcher_loop(Ctx &c, int dev) {
   }
 }
 
-// Enqueues every hop of one call (the caller holds the context: its `pending` flag is set).
+// Enqueues every hop of one call (the caller holds the context: its `pending` flag is set).  The
+// context's end event is recorded after the launches, also when a launch fails part way (the
+// kernels enqueued before the failure still run: retire() waits for them on this event).
 void Sampler::launch(Ctx &c, const Job &j, hipStream_t st) {
+  if (!c.end_ev) DGS_HIP(hipEventCreateWithFlags(&c.end_ev, hipEventDisableTiming));
+  try {
+    launch_hops(c, j, st);
+  } catch (...) {
+    (void)hipEventRecord(c.end_ev, st);
+    throw;
+  }
+  // recorded here (on the launcher thread when the call is asynchronous), so a consumer of the
+  // outputs only needs a stream wait on the caller's thread (ended_event)
+  DGS_HIP(hipEventRecord(c.end_ev, st));
+}
+
+void Sampler::launch_hops(Ctx &c, const Job &j, hipStream_t st) {
   const int64_t *seeds = j.seeds;
   const int64_t n_seeds = j.n_seeds;
   const int L = j.L;
@@ -457,14 +487,19 @@ void Sampler::launch(Ctx &c, const Job &j, hipStream_t st) {
     S = Count{fcap[h], d_uniq};
   }
   profile_end(st, 1);
-  // recorded here (on the launcher thread when the call is asynchronous), so a consumer of the
-  // outputs only needs a stream wait on the caller's thread (ended_event)
-  if (!c.end_ev) DGS_HIP(hipEventCreateWithFlags(&c.end_ev, hipEventDisableTiming));
-  DGS_HIP(hipEventRecord(c.end_ev, st));
+}
+
+// Lookup only: a missing context is an error (never created, never evicting another).
+std::shared_ptr<Sampler::Ctx> Sampler::ctx_find(hipStream_t st) {
+  std::lock_guard<std::mutex> g(ctx_mu_);
+  auto it = ctxs_.find(st);
+  return it == ctxs_.end() ? nullptr : it->second;
 }
 
 void Sampler::wait_ended(hipStream_t st, hipStream_t consumer) {
-  const std::shared_ptr<Ctx> cp = ctx_for(st);
+  const std::shared_ptr<Ctx> cp = ctx_find(st);
+  DGS_CHECK(cp, "wait_ended: this stream has no sampling context (no call was ended on it, or "
+                "its context was evicted: more than DGS_SAMPLER_MAX_CTX streams in use)");
   Ctx &c = *cp;
   std::lock_guard<std::mutex> g(c.mu);
   DGS_CHECK(!c.pending && c.end_ev, "wait_ended: no ended call on this stream");
@@ -475,7 +510,8 @@ void Sampler::wait_ended(hipStream_t st, hipStream_t consumer) {
 // host returns while the last relabel pass still runs (every consumer of the outputs is
 // ordered after it on the stream).  A failed kernel shows up through hipStreamQuery.
 void Sampler::sample_end(int L, int64_t *sizes, hipStream_t st) {
-  const std::shared_ptr<Ctx> cp = ctx_for(st);
+  const std::shared_ptr<Ctx> cp = ctx_find(st);
+  DGS_CHECK(cp, "sample_end: no call outstanding on this stream");
   Ctx &c = *cp;
   std::unique_lock<std::mutex> lk(c.mu);
   DGS_CHECK(c.pending, "sample_end: no call outstanding on this stream");
@@ -528,7 +564,8 @@ void Sampler::sample_end(int L, int64_t *sizes, hipStream_t st) {
 void Sampler::build_cache_rowtab(int64_t *tab, hipStream_t st) const {
   loctab_init_host(tab, num_nodes_, st);
   for (int d : rotation(rank_, world_))
-    loctab_assign(tab, (const int64_t *)nids_srv_->ptr(d), nids_srv_->items(d), d, st);
+    loctab_assign(tab, num_nodes_, (const int64_t *)nids_srv_->ptr(d), nids_srv_->items(d), d,
+                  st);
 }
 
 int64_t Sampler::cache_map_size() const {
@@ -574,9 +611,15 @@ FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_byt
   hipStream_t st = nullptr;
   h_data_.attach(data, num_rows * row_bytes);
   int64_t *nids = device_copy_ids(cache_nids, n_cache, st);
+  // a cached id outside [0, num_rows) is refused (the reference's hashmap would take it and
+  // its gather read out of bounds, feature_server.cc:10-61)
+  if (count_out_of_range(nids, n_cache, num_rows, st) != 0) {
+    (void)hipFree(nids);
+    DGS_CHECK(false, "cache_nids: an id is outside [0, num_rows)");
+  }
   void *block = nullptr;
   DGS_HIP(hipMalloc(&block, (size_t)(n_cache * row_bytes > 0 ? n_cache * row_bytes : 1)));
-  gather_plain(h_data_.dev, row_bytes, nids, 8, n_cache, block, st);
+  gather_plain(h_data_.dev, num_rows, row_bytes, nids, 8, n_cache, block, st);
   DGS_HIP(hipStreamSynchronize(st));
   feat_srv_ = P2PServer::adopt(block, n_cache, row_bytes);
 
@@ -594,7 +637,8 @@ FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_byt
   ftab_init(ftab, num_rows, h_data_.dev, row_bytes, st);
   align_or_ = (uintptr_t)h_data_.dev;
   for (int d : rotation(rank_, world_)) {
-    ftab_assign(ftab, (const int64_t *)lists[d], nbytes[d] / 8, feat_srv_->ptr(d), row_bytes, st);
+    ftab_assign(ftab, num_rows, (const int64_t *)lists[d], nbytes[d] / 8, feat_srv_->ptr(d),
+                row_bytes, st);
     align_or_ |= (uintptr_t)feat_srv_->ptr(d);
   }
   DGS_HIP(hipStreamSynchronize(st));
@@ -629,14 +673,19 @@ void FeatureServer::detect_strided(const std::vector<void *> &lists,
   wshift_ = sh;
 }
 
-FeatureServer::~FeatureServer() { delete feat_srv_; }
+FeatureServer::~FeatureServer() {
+  // gathers queued on any stream read the table, the cache blocks and the host view: they
+  // finish before those go
+  (void)hipDeviceSynchronize();
+  delete feat_srv_;
+}
 
 void FeatureServer::gather(const int64_t *nids, int64_t n, void *out, hipStream_t st,
                            const LabelTail *tail) const {
   if (wshift_ >= 0)
-    gather_strided(bases_, wshift_, row_bytes_, nids, n, out, st, tail);
+    gather_strided(bases_, wshift_, num_rows_, row_bytes_, nids, n, out, st, tail);
   else
-    gather_table(ftab_.as<int64_t>(), align_or_, row_bytes_, nids, n, out, st, tail);
+    gather_table(ftab_.as<int64_t>(), num_rows_, align_or_, row_bytes_, nids, n, out, st, tail);
 }
 
 }  // namespace dgs

@@ -144,8 +144,11 @@ class Sampler {
   // context holds relabel tables of 16 B per node plus scratch); the reference keeps no state
   // between calls (sampler.cc:146-166).
   std::shared_ptr<Ctx> ctx_for(hipStream_t st);
+  // the context of `st` if there is one (no creation, no eviction)
+  std::shared_ptr<Ctx> ctx_find(hipStream_t st);
   static void retire(Ctx &c);
   void launch(Ctx &c, const Job &j, hipStream_t st);
+  void launch_hops(Ctx &c, const Job &j, hipStream_t st);
   void launcher_loop(Ctx &c, int dev);
   std::mutex ctx_mu_;
   std::unordered_map<hipStream_t, std::shared_ptr<Ctx>> ctxs_;

@@ -19,14 +19,22 @@ from dgs._lib import _raw_stream
 
 __all__ = ["PrefetchLoader"]
 
-# Batch streams are pooled per device and checked out by one loader at a time: the sampler
-# keeps one sampling context (scratch, relabel tables: 16 B per node) per stream for its
-# lifetime and allows one outstanding call per stream, so two live loaders over one sampler
-# (zipped, nested, or one left open) must not share a stream.  A loader returns its streams in
-# close(); a stream's first use by the sampler allocates its context.
+# Batch streams are the library's own (dgs.ops._stream_create: non-blocking HIP streams that
+# nobody else is handed), pooled per device and checked out by one loader at a time.  torch's
+# pooled streams (torch.cuda.Stream()) would not do: torch hands the same 32 streams round robin
+# to every caller, so a batch stream could be the caller's current stream or another
+# component's, and with host-asynchronous launches the sampler's launcher thread would then
+# enqueue on a stream the caller also writes (include/dgs_amd.h, DGS_SAMPLE_HOST_ASYNC).  The
+# sampler keeps one sampling context (scratch, relabel tables: 16 B per node) per stream and
+# allows one outstanding call per stream, so two live loaders over one sampler (zipped, nested,
+# or one left open) must not share a stream either.  A loader returns its streams in close();
+# pooled streams live for the process.
 _FREE_STREAMS = {}
 # DGS_PREFETCH_SYNC=1: issue each batch's launches on the caller's thread (experiments)
 _HOST_ASYNC = os.environ.get("DGS_PREFETCH_SYNC", "0") != "1"
+# HIP priority of new batch streams (0 = default; -1 = high: their kernels are dispatched ahead
+# of the default-priority queues')
+_PRIORITY = int(os.environ.get("DGS_PREFETCH_STREAM_PRIORITY", "0"))
 _STREAMS_LOCK = threading.Lock()
 
 
@@ -35,7 +43,9 @@ def _checkout_streams(device, n):
         free = _FREE_STREAMS.setdefault(device, [])
         out = [free.pop() for _ in range(min(n, len(free)))]
     while len(out) < n:
-        out.append(torch.cuda.Stream(device=device))
+        with torch.cuda.device(device):
+            raw = dgs.ops._stream_create(_PRIORITY)
+        out.append(torch.cuda.ExternalStream(raw, device=device))
     return out
 
 
@@ -79,6 +89,7 @@ class PrefetchLoader:
             for d in labels.shape[1:]:
                 self._label_row_bytes *= int(d)
         self.fan_out, self.replace = list(fan_out), bool(replace)
+        self._streams = []  # (close() may run on a loader whose __init__ failed below)
         self._seeds = iter(seeds_iter)
         self._exhausted = False
         self._streams = _checkout_streams(self.device, depth)

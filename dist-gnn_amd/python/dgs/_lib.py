@@ -45,8 +45,11 @@ _SIGS = {
     "dgs_set_random_seed": (c_int, [c_u64]),
     "dgs_host_register": (c_int, [c_vp, c_i64]),
     "dgs_host_unregister": (c_int, [c_vp]),
-    "dgs_index_select": (c_int, [c_vp, c_i64, c_vp, c_int, c_i64, c_vp, c_vp]),
-    "dgs_index_select_device": (c_int, [c_vp, c_i64, c_vp, c_int, c_i64, c_vp, c_vp]),
+    "dgs_index_select": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_i64, c_vp, c_vp]),
+    "dgs_index_select_device": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_i64, c_vp, c_vp]),
+    "dgs_check_async_errors": (c_int, []),
+    "dgs_stream_create": (c_int, [c_int, p_vp]),
+    "dgs_stream_destroy": (c_int, [c_vp]),
     "dgs_stream_wait": (c_int, [c_vp, c_vp]),
     "dgs_stream_wait_event": (c_int, [c_vp, c_vp]),
     "dgs_sample_neighbors": (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_int, c_vp, c_vp,
@@ -73,8 +76,8 @@ _SIGS = {
     "dgs_sampler_sample_end": (c_int, [c_vp, c_int, p_i64, c_vp]),
     "dgs_sampler_sample_begin_after": (c_int, [c_vp, c_vp, c_vp, c_i64, p_i64, c_int, c_int,
                                                c_vp, ctypes.POINTER(c_u64), c_int, c_vp]),
-    "dgs_loader_gather": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
-                                  c_i64, c_vp]),
+    "dgs_loader_gather": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64,
+                                  c_vp, c_i64, c_vp]),
     "dgs_sampler_context_count": (c_int, [c_vp, p_i64]),
     "dgs_sampler_local_cache": (c_int, [c_vp, p_vp, p_i64, p_vp, p_i64, p_vp]),
     "dgs_sampler_cache_map_size": (c_int, [c_vp, p_i64]),

@@ -370,6 +370,8 @@ class _PendingSample:
             if self._L == 0:
                 self._out = []
             else:
+                if self._owner._h is None:  # destroyed (e.g. finalised first in a GC cycle)
+                    raise RuntimeError("dgs: the sampler of this call has been destroyed")
                 sizes = (c_i64 * (3 * self._L))()
                 check(lib.dgs_sampler_sample_end(self._owner._h, self._L, sizes, self._stream))
                 self._out = self._owner._views(self._seeds, self._buf, self._caps, self._total,

@@ -225,7 +225,8 @@ def _CAPI_cuda_index_select(data, nid):
     _, rb = row_bytes(d)
     dev = n.device if n.is_cuda else _cuda_dev()
     out = torch.empty((n.numel(),) + tuple(d.shape[1:]), dtype=d.dtype, device=dev)
-    check(lib.dgs_index_select(ptr(d), rb, ptr(n), n.element_size(), n.numel(), ptr(out),
+    rows = d.shape[0] if d.dim() > 0 else 1
+    check(lib.dgs_index_select(ptr(d), rows, rb, ptr(n), n.element_size(), n.numel(), ptr(out),
                                stream_ptr(dev)))
     return out
 
@@ -236,7 +237,7 @@ def _index_select_into(data, nid, out, stream):
     rb = data.element_size()
     for d in data.shape[1:]:
         rb *= int(d)
-    check(lib.dgs_index_select_device(ctypes.c_void_p(data.data_ptr()), rb,
+    check(lib.dgs_index_select_device(ctypes.c_void_p(data.data_ptr()), data.shape[0], rb,
                                       ctypes.c_void_p(nid.data_ptr()), 8, nid.numel(),
                                       ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream)))
 
@@ -252,9 +253,27 @@ def _loader_gather(sampler, server, producer, consumer, nids, x, labels, label_r
         server._h if server is not None else None, producer, consumer,
         nids.data_ptr() if nids is not None else None, nids.numel() if nids is not None else 0,
         x.data_ptr() if x is not None else None,
-        labels.data_ptr() if labels is not None else None, label_row_bytes,
+        labels.data_ptr() if labels is not None else None,
+        labels.shape[0] if labels is not None else 0, label_row_bytes,
         seeds.data_ptr(), seeds.numel() if labels is not None else 0,
         y.data_ptr() if y is not None else None))
+
+
+def _check_async_errors():
+    """ADDITIVE: raises RuntimeError if a gather kernel of this process met an id outside its
+    source's rows since the last check (the kernel read row 0 instead; the reference reads out
+    of bounds).  Every gather entry point checks this first, so such an error surfaces at the
+    next gather at the latest.  No synchronisation: synchronise first to see queued work's."""
+    check(lib.dgs_check_async_errors())
+
+
+def _stream_create(priority=0):
+    """ADDITIVE: a new non-blocking HIP stream (int handle) owned by the caller; hand it to
+    torch with torch.cuda.ExternalStream.  Unlike torch's pooled streams it is never given to
+    anyone else."""
+    out = ctypes.c_void_p()
+    check(lib.dgs_stream_create(int(priority), ctypes.byref(out)))
+    return out.value
 
 
 def _stream_wait(producer, consumer):

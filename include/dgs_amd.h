@@ -81,14 +81,26 @@ int dgs_host_unregister(void *ptr);
  * Stateless ops (pybind.cc:53-76)
  * ---------------------------------------------------------------------------------- */
 /* replaces feature::cuda::GetFeaturesCUDA (feature_ops.cu:140-210; _CAPI_cuda_index_select):
- * out[i, :] = data[nid[i], :] as a byte copy of row_bytes per row. nid_bytes = 4 | 8. */
-int dgs_index_select(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
-                     int64_t n, void *out, void *stream);
+ * out[i, :] = data[nid[i], :] as a byte copy of row_bytes per row; data has num_rows rows.
+ * nid_bytes = 4 | 8.  Range guard (every gather of this header): an id outside [0, num_rows)
+ * -- which the reference reads out of bounds -- fills its row from row 0 instead, and the next
+ * gather entry point of the process (or dgs_check_async_errors) returns -1 naming the id. */
+int dgs_index_select(const void *data, int64_t num_rows, int64_t row_bytes, const void *nid,
+                     int nid_bytes, int64_t n, void *out, void *stream);
 
 /* ADDITIVE: dgs_index_select for callers that know data and nid are device memory (no
  * pointer-attribute queries: the per-batch loader path). */
-int dgs_index_select_device(const void *data, int64_t row_bytes, const void *nid, int nid_bytes,
-                            int64_t n, void *out, void *stream);
+int dgs_index_select_device(const void *data, int64_t num_rows, int64_t row_bytes,
+                            const void *nid, int nid_bytes, int64_t n, void *out, void *stream);
+/* ADDITIVE: -1 (with the message) when a gather kernel of this process met an id outside its
+ * source's rows since the last check; clears the report.  No synchronisation: the report of a
+ * kernel still queued appears once it has run. */
+int dgs_check_async_errors(void);
+/* ADDITIVE: a non-blocking HIP stream owned by the caller (hipStreamCreateWithPriority;
+ * priority 0 = default, lower = higher priority), for a loader's batch streams: unlike a
+ * framework's pooled streams it is never handed to anyone else. */
+int dgs_stream_create(int priority, void **stream_out);
+int dgs_stream_destroy(void *stream);
 /* ADDITIVE: `consumer` waits (on the device) for the work enqueued on `producer` so far -- an
  * event record + stream wait in one call (DistGNN.dataloading.PrefetchLoader). */
 int dgs_stream_wait(void *producer, void *consumer);
@@ -159,7 +171,8 @@ int dgs_p2p_server_destroy(dgs_p2p_server *s); /* collective when world_size > 1
 typedef struct dgs_sampler dgs_sampler;
 /* indptr[num_nodes+1], indices[num_edges], probs[num_edges] or NULL: host arrays (registered
  * by the library when not already pinned) -- sampler.cc:64-136.  cache_nids: this rank's
- * cached node ids (device or host).  Collective when world_size > 1. */
+ * cached node ids (device or host; an id outside [0, num_nodes) is refused).  Collective when
+ * world_size > 1.  Destruction waits for the sampler's calls and the device's queued work. */
 int dgs_sampler_create(const int64_t *indptr, const int64_t *indices, const float *probs,
                        int64_t num_nodes, int64_t num_edges, const int64_t *cache_nids,
                        int64_t n_cache, int64_t device_id, dgs_sampler **out);
@@ -207,7 +220,8 @@ int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_see
 int dgs_sampler_sample_end(dgs_sampler *s, int L, int64_t *sizes_out, void *stream);
 /* ADDITIVE: with DGS_SAMPLE_WAIT in `flags`, `stream` first waits for the work enqueued on
  * `wait_for` so far (any stream, NULL = the null stream); with DGS_SAMPLE_WAIT_EVENT it waits on
- * the event `wait_for`; then dgs_sampler_sample_begin with
+ * the event `wait_for`; a non-NULL `wait_for` without either flag is an error (round 3's
+ * header waited whenever it was non-NULL); then dgs_sampler_sample_begin with
  * every hop's outputs packed in one device buffer `out`:
  * per hop h, frontier[fcap_h], rows[ecap_h], cols[ecap_h] back to back (the capacities of
  * dgs_sampler_bounds) -- one call per batch for a pipelined loader.  `seeds` must be device
@@ -240,7 +254,8 @@ int dgs_sampler_destroy(dgs_sampler *s); /* collective when world_size > 1 */
  * ---------------------------------------------------------------------------------- */
 typedef struct dgs_feature_server dgs_feature_server;
 /* data: host array [num_rows, row_bytes] (registered by the library when not pinned);
- * cache_nids: rows cached in this GPU's HBM (device or host).  feature_server.cc:10-61. */
+ * cache_nids: rows cached in this GPU's HBM (device or host; an id outside [0, num_rows) is
+ * refused).  feature_server.cc:10-61.  Destruction waits for the device's queued work. */
 int dgs_feature_server_create(const void *data, int64_t num_rows, int64_t row_bytes,
                               const int64_t *cache_nids, int64_t n_cache, int64_t device_id,
                               dgs_feature_server **out);
@@ -255,15 +270,16 @@ int dgs_feature_server_local_cache(const dgs_feature_server *s, const void **ptr
 int dgs_stream_wait_event(void *event, void *consumer);
 /* ADDITIVE (PrefetchLoader, one call per batch): `consumer` waits for `producer` (the batch's
  * sample call), then on `consumer` the feature gather of nids[n] into feat_out (fs may be
- * NULL) and, when labels != NULL, label_out[i] = labels[seeds[i]] (rows of label_row_bytes,
- * int64 seeds).  nids, seeds and every buffer are device memory.  With s != NULL the call on
+ * NULL) and, when labels != NULL, label_out[i] = labels[seeds[i]] (label_rows rows of
+ * label_row_bytes, int64 seeds; both gathers range-guarded as dgs_index_select).  nids, seeds
+ * and every buffer are device memory.  With s != NULL the call on
  * `producer` must have been ended (dgs_sampler_sample_end) and no new one begun: `consumer`
  * waits on the event that call's launches recorded, with no event record here; with s == NULL
  * an event is recorded on `producer` now. */
 int dgs_loader_gather(dgs_sampler *s, dgs_feature_server *fs, void *producer, void *consumer,
                       const int64_t *nids, int64_t n, void *feat_out, const void *labels,
-                      int64_t label_row_bytes, const int64_t *seeds, int64_t n_seeds,
-                      void *label_out);
+                      int64_t label_rows, int64_t label_row_bytes, const int64_t *seeds,
+                      int64_t n_seeds, void *label_out);
 /* ADDITIVE.  Address layout the gather uses: -1 = per-node address table (general cache
  * placement), w >= 0 = every node cached in the strided layout (node v at row v >> w of GPU
  * v & (2^w - 1); w = 0 is the whole-graph-in-HBM identity), no per-node table read. */

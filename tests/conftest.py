@@ -25,3 +25,22 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _gpu_test_drained(request):
+    """After every GPU test: collect garbage (services finalised in GC cycles are destroyed
+    here, not inside a later test), drain the device and check the library's async error
+    report.  A fault or an out-of-range gather is then attributed to the test that caused it
+    (an asynchronous HIP error otherwise surfaces at whatever call comes next)."""
+    yield
+    if "gpu" not in request.keywords:
+        return
+    import gc
+    import torch
+    if not torch.cuda.is_available():
+        return
+    gc.collect()
+    torch.cuda.synchronize()
+    import dgs
+    dgs.ops._check_async_errors()
