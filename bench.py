@@ -104,10 +104,22 @@ def parse(argv=None):
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--seed", type=int, default=20261015)
+    p.add_argument("--secondary", choices=["auto", "none", "papers_bias"], default="auto",
+                   help="N = 1: also measure configs[3] (papers100M-like, biased) as a nested "
+                        "record (auto: when the primary workload is the default one)")
     a = p.parse_args(argv)
     if a.shard:
         a.mode = "shard"
     return a
+
+
+def baseline_config(args, mode, hot):
+    """The BASELINE.json config this run's workload stands for."""
+    if hot is not None:
+        return "SURVEY 8(f) rank 2"
+    if (args.scale, args.ef) == (27, 12) and args.bias and mode == "replicated":
+        return "configs[3] (its graph and sampler, on one GPU)"
+    return CONFIG_OF_MODE[mode]
 
 
 def workload_name(scale, ef):
@@ -386,6 +398,51 @@ def main():
             dgs.ops._CAPI_set_host_comm(dist.group.WORLD if share
                                         else dist.new_group(backend="gloo"))
 
+    out = run_workload(args, dgs, dist, world, rank, local_rank, mode, share, dev_index, dev, comm)
+    sec = secondary_workload(args, world)
+    if sec is not None:
+        # configs[3] (papers100M-like graph, degree-weighted biased [15,10,5], d = 128) in the
+        # same run: the north star's own sampler config, on one GPU
+        a2 = parse(sys.argv[1:])
+        for k, v in sec.items():
+            setattr(a2, k, v)
+        t_sec = time.time()
+        try:
+            rec = run_workload(a2, dgs, dist, world, rank, local_rank, "replicated", share,
+                               dev_index, dev, comm)
+            rec["wall_s"] = time.time() - t_sec
+        except (RuntimeError, MemoryError, torch.OutOfMemoryError) as e:  # reported, not fatal
+            rec = {"skipped": f"{type(e).__name__}: {e}"[:400]}
+            torch.cuda.empty_cache()
+        out["secondary"] = {"papers_bias": rec}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def secondary_workload(args, world):
+    """--secondary auto: the N = 1 default run (products-like uniform, configs[1]) also measures
+    configs[3]'s sampler -- papers100M-like RMAT scale 27 x ef 12 (134 M nodes, 1.61 B edges),
+    degree-weighted biased [15,10,5], d = 128 -- as a nested record of the same JSON line, with
+    the same steps / warm-up and a shorter CPU baseline.  Returns the argument overrides, or
+    None."""
+    if args.secondary == "none" or world != 1:
+        return None
+    default = (args.scale, args.ef, args.dim, args.bias, args.cache_frac) == (21, 59, 100, False,
+                                                                              1.0)
+    if args.secondary == "auto" and not default:
+        return None
+    return {"scale": 27, "ef": 12, "dim": 128, "bias": True, "mode": "replicated",
+            "seq_calls": min(args.seq_calls, 20),
+            "cpu_baseline_seconds": min(args.cpu_baseline_seconds, 8.0), "secondary": "none"}
+
+
+def run_workload(args, dgs, dist, world, rank, local_rank, mode, share, dev_index, dev, comm):
+    """One workload's bench record: inputs, services, self-check (N > 1), the timed pass, side
+    passes and the CPU baseline; the services and inputs are freed before returning."""
     fan_out = [int(x) for x in args.fan_out.split(",")]
 
     # ---------------- synthetic inputs (identical on every rank)
@@ -535,7 +592,7 @@ def main():
                          f"{sampler_kind} sampler fan-out {fan_out} without replacement, "
                          f"B={args.batch} seeds/step/GPU, + feature gather d={args.dim} f32 + "
                          f"label gather; {placement}"),
-            "baseline_config": CONFIG_OF_MODE[mode] if hot is None else "SURVEY 8(f) rank 2",
+            "baseline_config": baseline_config(args, mode, hot),
             "mode": mode,
             "fan_out": fan_out, "batch_per_gpu": args.batch, "num_nodes": N, "num_edges": E,
             "feat_dim": args.dim, "parallelism": f"dp{world} (seed-parallel)",
@@ -609,15 +666,13 @@ def main():
         out["roofline"]["xgmi_bound_GBps"] = 2 * world * XGMI_LINK_GBPS
         out["roofline"]["frac_of_xgmi_bound"] = (None if share else
                                                  achieved / (2 * world * XGMI_LINK_GBPS))
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    # collective destructors (same order on every rank) before the group goes away
+    # collective destructors (same order on every rank) before the next workload / teardown
     del ref
     del sampler, server
+    del inp, indptr, indices, feats, labels, probs, labels_dev, local_mask, cached_mask
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-        dist.destroy_process_group()
+    torch.cuda.empty_cache()
+    return out
 
 
 def next_seeds_factory(train_local, args):

@@ -41,6 +41,8 @@ def main():
     for r in range(rounds):
         for lib in libs:
             cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline"] + extra
+            if "--secondary" not in extra:
+                cmd += ["--secondary", "none"]
             out = subprocess.run(cmd, env=variant_env(lib), capture_output=True, text=True,
                                  timeout=int(os.environ.get("AB_TIMEOUT", "300")))
             if out.returncode != 0:

@@ -31,7 +31,7 @@ for step in "$@"; do
         --warmup 10 > $O/bench_$step.json 2> $O/bench_$step.err; rc=$?
       tail -3 $O/bench_$step.err; cut -c1-300 $O/bench_$step.json; ok $rc ;;
     bench)
-      timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err; rc=$?
+      timeout -k 10 500 python bench.py ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err; rc=$?
       cut -c1-300 $O/bench.json; ok $rc ;;
     bias)
       timeout -k 10 300 python bench.py --bias --no-cpu-baseline > $O/bench_bias.json \
@@ -41,13 +41,25 @@ for step in "$@"; do
         > $O/bench_papers.json 2> $O/bench_papers.err; rc=$?; cut -c1-300 $O/bench_papers.json; ok $rc ;;
     papersbias)
       timeout -k 10 600 python bench.py --scale 27 --ef 12 --dim 128 --bias --no-cpu-baseline \
-        > $O/bench_papers_bias.json 2> $O/bench_papers_bias.err; rc=$?
-      cut -c1-300 $O/bench_papers_bias.json; ok $rc ;;
+        ${PB_ARGS:-} > $O/bench_papers_bias.json 2> $O/bench_papers_bias.err; rc=$?
+      cut -c1-300 $O/bench_papers_bias.json; tail -8 $O/bench_papers_bias.err; ok $rc ;;
+    driverbench)
+      # the driver's own command, timed
+      t0=$(date +%s.%N)
+      timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 \
+        > $O/driver_bench.json 2> $O/driver_bench.err; rc=$?
+      echo "driver bench wall: $(python3 -c "import time; print(round(time.time() - $t0, 1))") s" | tee $O/driver_bench_wall.txt
+      cut -c1-300 $O/driver_bench.json; tail -12 $O/driver_bench.err; ok $rc ;;
     rocprof)
       (cd /tmp && export TMPDIR=/tmp) ; export TMPDIR=/tmp
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py \
         --no-cpu-baseline > $O/bench_rocprof.json 2> $O/bench_rocprof.err; rc=$?
       cut -c1-200 $O/bench_rocprof.json; ok $rc ;;
+    detail)
+      # workgroup stamps of the gather and hub kernels inside the pipeline (DGS_PROF_DETAIL)
+      DGS_PROF_DETAIL=1 DGS_PROF_HUB=1 timeout -k 10 600 python bench.py --no-cpu-baseline \
+        --secondary none ${DETAIL_ARGS:-} > $O/detail.json 2> $O/detail.err; rc=$?
+      grep "dgs prof" $O/detail.err | tail -12; ok $rc ;;
     ab)
       # same-box A/B: AB_VARIANTS (space-separated ab_bench variants), AB_ARGS (bench args)
       timeout -k 10 1000 python tools/ab_bench.py --rounds ${AB_ROUNDS:-3} -- $AB_VARIANTS \
