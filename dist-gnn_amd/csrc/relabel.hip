@@ -10,8 +10,6 @@
 // hash, linear probing at load factor <= 0.5 in a table sized for this hop (it stays in the
 // L2 / Infinity Cache at the benchmark sizes).  The table is persistent and is cleaned by
 // the relabel pass itself (only the slots this hop touched), so no per-hop memset.
-#include <cstdlib>
-
 #include "dgs_block.cuh"
 #include "dgs_ops.h"
 #include "dgs_table.cuh"
@@ -231,68 +229,6 @@ __global__ __launch_bounds__(kThreads) void k_dscatter(const int64_t *a, Count n
   }
 }
 
-// Small hops (cat(seeds, col) of at most kOneTile elements: the first hop of a 1024-seed batch):
-// count and scatter in ONE workgroup -- flags, one block scan, scatter -- with no tile counts in
-// memory and one launch fewer than k_dcount + k_dscatter (round 5).  Same flags, labels, id
-// checks and size publication as the two-pass form.
-constexpr int kOneThreads = 1024;
-constexpr int kOneItems = 8;
-constexpr int64_t kOneTile = (int64_t)kOneThreads * kOneItems;
-__global__ __launch_bounds__(kOneThreads) void k_dcompact_one(const int64_t *a, Count nac,
-                                                              const int64_t *b, const int64_t *d_nb,
-                                                              Table t, int64_t *unique,
-                                                              int64_t *d_nunique, HostSizes pub,
-                                                              IdCheck chk, const int64_t *rows) {
-  latency_prio();
-  __shared__ int64_t lds[kOneThreads / 64];
-  const int64_t na = nac.get();
-  const int64_t n = na + *d_nb;
-  const int64_t i0 = (int64_t)threadIdx.x * kOneItems;
-  int64_t x[kOneItems];
-  int32_t pv[kOneItems];
-  bool f[kOneItems];
-  // branch-free: every id load issues back to back, then every table load
-#pragma unroll
-  for (int j = 0; j < kOneItems; ++j) {
-    int64_t i = i0 + j < n ? i0 + j : n - 1;
-    i = i < 0 ? 0 : i;
-    x[j] = n > 0 ? (i < na ? a[i] : b[i - na]) : 0;
-  }
-#pragma unroll
-  for (int j = 0; j < kOneItems; ++j)
-    pv[j] = (uint64_t)x[j] < (uint64_t)t.n ? *dval(t, x[j]) : kNoPos;
-  int64_t cnt = 0;
-#pragma unroll
-  for (int j = 0; j < kOneItems; ++j) {
-    f[j] = i0 + j < n && pv[j] == (int32_t)(i0 + j);
-    cnt += f[j];
-  }
-  if (chk.bad) {
-#pragma unroll
-    for (int j = 0; j < kOneItems; ++j) {
-      const int64_t i = i0 + j;
-      if (i < na || i >= n) continue;
-      const int64_t row = rows ? rows[i - na] : 0;
-      if ((uint64_t)x[j] >= (uint64_t)t.n || (uint64_t)row >= (uint64_t)na)
-        report_bad_id(chk, i - na, x[j], n - na, rows ? row : -1);
-    }
-  }
-  int64_t tot;
-  int64_t ex = block_exclusive_scan<kOneThreads>(cnt, &tot, lds);
-#pragma unroll
-  for (int j = 0; j < kOneItems; ++j) {
-    if (f[j]) {
-      unique[ex] = x[j];
-      *dlab(t, x[j]) = (int32_t)ex;
-      ++ex;
-    }
-  }
-  if (threadIdx.x == 0) {
-    *d_nunique = tot;
-    publish_sizes(pub);
-  }
-}
-
 __global__ __launch_bounds__(kThreads) void k_drelabel_hop(RelabelTail r) {
   latency_prio();
   relabel_tail_block(r, blockIdx.x);
@@ -382,26 +318,6 @@ void relabel_hop(const int64_t *seeds, Count Sc, const int64_t *col, const int64
   ws.misc.ensure(sizeof(int64_t) * (size_t)(2 * nblk + 2));
   int64_t *bcnt = ws.misc.as<int64_t>();
   int64_t *boff = bcnt + nblk;
-  // DGS_COMPACT_ONE=0 turns the single-workgroup form for small hops off (A/B)
-  static const bool one_ok = [] {
-    const char *e = getenv("DGS_COMPACT_ONE");
-    return !(e && e[0] == '0');
-  }();
-  if (t.direct && one_ok && n_ub <= kOneTile) {
-    hipLaunchKernelGGL(k_dcompact_one, dim3(1), dim3(kOneThreads), 0, st, seeds, Sc, col, d_nnz,
-                       t, unique, d_nunique, pub, chk,
-                       seeds_unique ? (const int64_t *)nullptr : (const int64_t *)out_row);
-    DGS_LAUNCH_CHECK();
-    const RelabelTail tail{seeds, Sc, d_nnz, t, (int)!seeds_unique, out_row, out_col,
-                           unique, d_nunique, nblk, chk};
-    if (defer) {
-      *defer = tail;
-    } else {
-      hipLaunchKernelGGL(k_drelabel_hop, dim3((unsigned)nblk), dim3(kThreads), 0, st, tail);
-      DGS_LAUNCH_CHECK();
-    }
-    return;
-  }
   if (t.direct) {
     const int64_t ntiles = ceil_div(n_ub > 0 ? n_ub : 1, kCompactTile);
     int64_t *tcnt = bcnt;  // ws.misc holds >= nblk >= ntiles words
