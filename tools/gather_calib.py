@@ -11,7 +11,8 @@ import torch  # noqa: E402
 
 import dgs  # noqa: E402
 
-N, D, REPS = 1 << 22, 100, 5
+N, REPS = 1 << 22, 5
+D = int(os.environ.get("DGS_PMC_DIM", "100"))  # the bench's feature width
 table = torch.randn(N, D, device="cuda")              # 1.68 GB, far beyond the 256 MB MALL
 nids = torch.arange(N, dtype=torch.int64, device="cuda")
 for _ in range(REPS):

@@ -67,7 +67,7 @@ def main(root):
     kernel_name = "k_gather<16, StridedSrc>" if any(
         "StridedSrc" in n for n in kernel_names(f"{root}/pmc_bench_fetch/**/*counter_collection.csv")
     ) else "k_gather<16, TableSrc>"
-    N, D = 1 << 22, 100
+    N, D = 1 << 22, int(os.environ.get("DGS_PMC_DIM", "100"))
     calib_read = N * (D * 4 + 8)          # rows + nids
     calib_write = N * D * 4
     cfetch = sorted(cf)[len(cf) // 2] * 1024
@@ -87,7 +87,7 @@ def main(root):
     write = wr_row * bench_rows if bench_rows else None
     out = {
         "kernel": kernel_name, "dim": D,
-        "calibration": {"workload": "sequential gather of 2^22 rows x 400 B (tools/gather_calib.py)",
+        "calibration": {"workload": f"sequential gather of 2^22 rows x {D * 4} B (tools/gather_calib.py)",
                         "expected_read_bytes": calib_read, "fetch_size_bytes": cfetch,
                         "read_factor": read_factor, "expected_write_bytes": calib_write,
                         "write_size_bytes": cwrite, "write_factor": write_factor},

@@ -25,7 +25,7 @@ for step in "$@"; do
       rc=$?; tail -2 $O/smoke.log; ok $rc ;;
     probe)
       RUNS=${RUNS:-3} bash tools/r04_n2_probe.sh $N/n2; ok $? ;;
-    n2|n4)
+    n2|n4|n8)
       k=${step#n}
       DGS_BENCH_SHARE_DEVICE=1 timeout -k 10 400 python bench.py --gpus $k --steps 300 \
         --warmup 10 > $O/bench_$step.json 2> $O/bench_$step.err; rc=$?
@@ -53,7 +53,7 @@ for step in "$@"; do
     rocprof)
       (cd /tmp && export TMPDIR=/tmp) ; export TMPDIR=/tmp
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py \
-        --no-cpu-baseline > $O/bench_rocprof.json 2> $O/bench_rocprof.err; rc=$?
+        --no-cpu-baseline --secondary none ${PROF_ARGS:-} > $O/bench_rocprof.json 2> $O/bench_rocprof.err; rc=$?
       cut -c1-200 $O/bench_rocprof.json; ok $rc ;;
     detail)
       # workgroup stamps of the gather and hub kernels inside the pipeline (DGS_PROF_DETAIL)
