@@ -36,6 +36,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--scale 
                        [--bias] [--cache-frac f]
 """
 import argparse
+import gc
 import json
 import math
 import os
@@ -321,6 +322,11 @@ def timed_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist
         dgs.ops.profile_enable(dgs.ops.PROFILE_GATHER)
     seg0 = torch.cuda.memory_stats(dev).get("segment.all.allocated", 0)
     edges = rows = 0
+    # Python's cyclic garbage collector is held off inside the timed region: a full collection
+    # over torch's object graph stalls the host for milliseconds (a 10 ms step gap was seen in a
+    # 1000-step run), which a 20-step run cannot absorb.  No GPU work depends on it.
+    gc.collect()
+    gc.disable()
     t0 = time.perf_counter()
     step_t = []
     for blocks, x, _ in it:
@@ -332,6 +338,7 @@ def timed_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     prof = dgs.ops.profile_read() if profile else None
     # hipMalloc calls the caching allocator made inside the timed region (host stalls)
     mallocs = torch.cuda.memory_stats(dev).get("segment.all.allocated", 0) - seg0
@@ -612,6 +619,7 @@ def run_workload(args, dgs, dist, world, rank, local_rank, mode, share, dev_inde
         # timed region; a mismatch ends the run non-zero on every rank)
         "self_check": self_check,
         "host_step_gap_ms": step_gaps,
+        "python_gc_in_timed_region": "disabled (gc.collect() before, gc.enable() after)",
         "allocator_mallocs_in_timed_region": mallocs,
         "host_row_share": side["host_rows"],
         # gathered rows that cached on another GPU (read over xGMI)
