@@ -174,3 +174,22 @@ def test_compare_batches_counts_mismatches():
     assert bench.compare_batches(good, [(b2, x, y)]) == 1
     assert bench.compare_batches(good, [(b, x + 1, y)]) == 1
     assert bench.compare_batches(good, []) == 1
+
+
+def test_secondary_papers_bias_record_only_for_the_default_single_gpu_run():
+    """The default N = 1 run adds configs[3] (papers-like graph, degree-weighted biased sampler,
+    d = 128) as a nested record; any other workload, N > 1, or --secondary none does not."""
+    sec = bench.secondary_workload(bench.parse([]), 1)
+    assert sec["scale"] == 27 and sec["ef"] == 12 and sec["dim"] == 128 and sec["bias"]
+    assert sec["secondary"] == "none" and sec["mode"] == "replicated"
+    assert bench.secondary_workload(bench.parse([]), 2) is None
+    assert bench.secondary_workload(bench.parse(["--bias"]), 1) is None
+    assert bench.secondary_workload(bench.parse(["--secondary", "none"]), 1) is None
+    assert bench.secondary_workload(bench.parse(["--scale", "17", "--secondary", "papers_bias"]),
+                                    1) is not None
+    a2 = bench.parse([])
+    for k, v in sec.items():
+        setattr(a2, k, v)
+    assert bench.baseline_config(a2, "replicated", None).startswith("configs[3]")
+    assert bench.baseline_config(bench.parse([]), "replicated", None) == "configs[1]"
+    assert bench.baseline_config(bench.parse([]), "hot-shard", None) == "configs[2]"

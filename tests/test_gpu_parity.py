@@ -121,7 +121,10 @@ def _bias_hub_graph(seed):
     rows with infinite weights (tied keys), plus ordinary rows."""
     rng = np.random.default_rng(seed)
     degs = rng.integers(0, 60, 300)
-    hubs = [2049, 3000, 5000, 8192, 8193, 9000, 20000, 30000, 70000, 250000]
+    # (round 5: rows of 3800 / 4000 edges have exactly the 16 chunks the boot draws -- nothing
+    # left for the stream -- and 4020 / 4300 leave one / two chunks to it)
+    hubs = [2049, 3000, 5000, 8192, 8193, 9000, 20000, 30000, 70000, 250000, 3800, 4000, 4020,
+            4300]
     degs[:len(hubs)] = hubs
     indptr = np.concatenate([[0], np.cumsum(degs)]).astype(np.int64)
     indices = rng.integers(0, degs.size, int(indptr[-1])).astype(np.int64)
