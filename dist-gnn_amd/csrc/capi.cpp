@@ -330,9 +330,11 @@ int dgs_sample_neighbors(const int64_t *seeds, int64_t Sn, const int64_t *indptr
     HopScratch *wsp = nullptr;
     const OpScratchLease lk = op_scratch(st, &wsp);
     HopScratch &ws = *wsp;
-    int64_t *tmp = nullptr;  // [0] = nnz, then rowpos[S*k]
+    // [0] = nnz, then rowpos[S*k]: the stream's op scratch (the library does not use the
+    // stream-ordered allocator)
     const int64_t cap = Sn * num_picks;
-    DGS_HIP(hipMallocAsync((void **)&tmp, sizeof(int64_t) * (size_t)(cap + 1), st));
+    ws.op_tmp.ensure(sizeof(int64_t) * (size_t)(cap + 1));
+    int64_t *tmp = ws.op_tmp.as<int64_t>();
     const Table no_table{nullptr, nullptr, nullptr, nullptr, 0};
     sample_hop(src, seeds, Count{Sn, nullptr}, num_picks, replace != 0, probs != nullptr,
                rng().next(), tmp + 1, out_col, tmp, no_table, ws, st);
@@ -340,7 +342,6 @@ int dgs_sample_neighbors(const int64_t *seeds, int64_t Sn, const int64_t *indptr
     DGS_HIP(hipMemcpyAsync(&nnz, tmp, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     DGS_HIP(hipStreamSynchronize(st));
     take_i64(seeds, tmp + 1, nnz, out_row, st);
-    DGS_HIP(hipFreeAsync(tmp, st));
     *nnz_out = nnz;
   });
 }
@@ -353,8 +354,11 @@ int dgs_relabel(const int64_t *const *maps, const int64_t *map_sizes, int n_maps
     int64_t nm = 0, nr = 0;
     for (int i = 0; i < n_maps; ++i) nm += map_sizes[i];
     for (int i = 0; i < n_reqs; ++i) nr += req_sizes[i];
-    int64_t *buf = nullptr;  // mapping[nm] | req[nr] | req_out[nr] | count
-    DGS_HIP(hipMallocAsync((void **)&buf, sizeof(int64_t) * (size_t)(nm + 2 * nr + 1), st));
+    HopScratch *ws = nullptr;
+    const OpScratchLease lk = op_scratch(st, &ws);
+    // mapping[nm] | req[nr] | req_out[nr] | count, in the stream's op scratch
+    ws->op_tmp.ensure(sizeof(int64_t) * (size_t)(nm + 2 * nr + 1));
+    int64_t *buf = ws->op_tmp.as<int64_t>();
     int64_t off = 0;
     for (int i = 0; i < n_maps; ++i) {
       if (map_sizes[i] > 0)
@@ -369,8 +373,6 @@ int dgs_relabel(const int64_t *const *maps, const int64_t *map_sizes, int n_maps
       off += req_sizes[i];
     }
     int64_t *d_cnt = buf + nm + 2 * nr;
-    HopScratch *ws = nullptr;
-    const OpScratchLease lk = op_scratch(st, &ws);
     relabel_generic(buf, nm, buf + nm, nr, unique_out, buf + nm + nr, d_cnt, *ws, st);
     off = nm + nr;
     for (int i = 0; i < n_reqs; ++i) {
@@ -382,7 +384,6 @@ int dgs_relabel(const int64_t *const *maps, const int64_t *map_sizes, int n_maps
     int64_t u = 0;
     DGS_HIP(hipMemcpyAsync(&u, d_cnt, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     DGS_HIP(hipStreamSynchronize(st));
-    DGS_HIP(hipFreeAsync(buf, st));
     *n_unique = u;
   });
 }
@@ -435,21 +436,13 @@ int dgs_compute_frontier_heat_fixed(const int64_t *seeds, int64_t n_seeds,
                                     float *frontier_heat, void *stream) {
   return guard([&] {
     hipStream_t st = S(stream);
-    // the int64 accumulator is this call's own (stream-ordered allocation, freed behind the
-    // kernels that use it): nothing another op or stream runs can overwrite it
-    unsigned long long *acc = nullptr;
-    DGS_HIP(hipMallocAsync((void **)&acc,
-                           sizeof(uint64_t) * (size_t)(num_nodes > 0 ? num_nodes : 1), st));
-    try {
-      heat(dev_ptr(seeds, "seeds"), n_seeds, dev_ptr(indptr, "indptr"),
-           dev_ptr(indices, "indices"), dev_ptr(probs, "probs"),
-           dev_ptr(seeds_heat, "seeds_heat"), num_picks, indptr_diff, frontier_heat, num_nodes,
-           acc, st);
-    } catch (...) {
-      (void)hipFreeAsync(acc, st);
-      throw;
-    }
-    DGS_HIP(hipFreeAsync(acc, st));
+    // the int64 accumulator is this call's own allocation, freed once the stream has run the
+    // kernels that use it: nothing another op or stream runs can overwrite it
+    TmpBuf acc(sizeof(uint64_t) * (size_t)(num_nodes > 0 ? num_nodes : 1), st);
+    heat(dev_ptr(seeds, "seeds"), n_seeds, dev_ptr(indptr, "indptr"),
+         dev_ptr(indices, "indices"), dev_ptr(probs, "probs"),
+         dev_ptr(seeds_heat, "seeds_heat"), num_picks, indptr_diff, frontier_heat, num_nodes,
+         acc.as<unsigned long long>(), st);
   });
 }
 

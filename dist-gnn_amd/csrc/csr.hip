@@ -166,10 +166,8 @@ void extract_indptr(const int64_t *nids, int64_t n, const int64_t *indptr, int64
                        indptr, sub_indptr);
     DGS_LAUNCH_CHECK();
   }
-  void *scratch = nullptr;
-  DGS_HIP(hipMallocAsync(&scratch, scan_scratch_bytes(n), st));
-  scan_exclusive(sub_indptr, n, sub_indptr, scratch, st);
-  DGS_HIP(hipFreeAsync(scratch, st));
+  TmpBuf scratch(scan_scratch_bytes(n), st);
+  scan_exclusive(sub_indptr, n, sub_indptr, scratch.p, st);
 }
 
 void extract_edge_data(const int64_t *nids, int64_t n, const int64_t *indptr,
@@ -253,21 +251,17 @@ void heat(const int64_t *seeds, int64_t n_seeds, const int64_t *indptr, const in
 
 void cache_map_compact(const int64_t *tab, int64_t n, int64_t *key, int64_t *idx,
                        int64_t *devid, int64_t *d_count, hipStream_t st) {
-  int64_t *pos = nullptr;
-  void *scratch = nullptr;
-  DGS_HIP(hipMallocAsync((void **)&pos, sizeof(int64_t) * (size_t)(n + 1), st));
-  DGS_HIP(hipMallocAsync(&scratch, scan_scratch_bytes(n), st));
+  TmpBuf posb(sizeof(int64_t) * (size_t)(n + 1), st), scratch(scan_scratch_bytes(n), st);
+  int64_t *pos = posb.as<int64_t>();
   if (n > 0) {
     hipLaunchKernelGGL(k_cached_flag, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, tab,
                        n, pos);
     DGS_LAUNCH_CHECK();
   }
-  scan_exclusive(pos, n, pos, scratch, st);
+  scan_exclusive(pos, n, pos, scratch.p, st);
   hipLaunchKernelGGL(k_cached_scatter, dim3((unsigned)ceil_div(n > 0 ? n : 1, 256)), dim3(256),
                      0, st, tab, n, pos, key, idx, devid, d_count);
   DGS_LAUNCH_CHECK();
-  DGS_HIP(hipFreeAsync(scratch, st));
-  DGS_HIP(hipFreeAsync(pos, st));
 }
 
 void loctab_init_host(int64_t *tab, int64_t n, hipStream_t st) {

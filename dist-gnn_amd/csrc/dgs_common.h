@@ -59,6 +59,27 @@ struct DevBuf {
   }
 };
 
+// Temporary device buffer of a setup-time or synchronous call: hipMalloc now; on scope exit the
+// stream is synchronised, then hipFree.  (The library keeps away from the stream-ordered
+// allocator, hipMallocAsync / hipFreeAsync: see DESIGN.md section 3.)
+struct TmpBuf {
+  void *p = nullptr;
+  hipStream_t st = nullptr;
+  TmpBuf(size_t bytes, hipStream_t s) : st(s) { DGS_HIP(hipMalloc(&p, bytes ? bytes : 1)); }
+  TmpBuf(const TmpBuf &) = delete;
+  TmpBuf &operator=(const TmpBuf &) = delete;
+  ~TmpBuf() {
+    if (p) {
+      (void)hipStreamSynchronize(st);
+      (void)hipFree(p);
+    }
+  }
+  template <typename T>
+  T *as() const {
+    return reinterpret_cast<T *>(p);
+  }
+};
+
 // Pinned host staging for small D2H size reads.
 struct HostPinned {
   void *p = nullptr;

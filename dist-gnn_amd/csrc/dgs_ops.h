@@ -109,6 +109,7 @@ struct RowSrc {
 struct HopScratch {
   DevBuf rowinfo, tpre, bsum, boff, hub, hubcount, hubslot, rowpos, slot_of, tkey, tval, tlab,
       misc, cdf, cand, flags;
+  DevBuf op_tmp;  // the standalone ops' call buffers (sample_neighbors, relabel)
   HostPinned host;
   uint64_t table_cap = 0;  // capacity currently allocated and clean
   uint64_t hop_serial = 0;  // parity selects the hub counter of a hop
