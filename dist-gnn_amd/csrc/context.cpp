@@ -181,7 +181,15 @@ void release_locked(const void *p) {
   auto it = host_reg_find(p);
   if (it == host_regs().end()) return;
   if (--it->second.refs == 0) {
-    (void)hipHostUnregister(reinterpret_cast<void *>(it->first));
+    // A failed unregister would leave HIP's mapping of pages the caller is about to free: a
+    // later allocation at the same addresses would then be taken for registered memory.  It
+    // cannot be raised from here (destructors), so it is reported.
+    const hipError_t e = hipHostUnregister(reinterpret_cast<void *>(it->first));
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      fprintf(stderr, "[dgs] warning: hipHostUnregister(%p, %zu bytes) failed: %s\n",
+              reinterpret_cast<void *>(it->first), it->second.bytes, hipGetErrorString(e));
+    }
     host_regs().erase(it);
   }
 }
