@@ -639,9 +639,10 @@ def run_workload(args, dgs, dist, world, rank, local_rank, mode, share, dev_inde
         "roofline": {
             "bound": ("hbm" if world == 1 or mode == "replicated"
                       else "hbm (local rows) + xGMI (remote rows)"),
-            "kernel": ("k_gather<16, StridedSrc> (P2PCacheFeatureServer gather, computed row "
+            "kernel": ("k_gather<16, U, StridedSrc> (P2PCacheFeatureServer gather, computed row "
                        "addresses)" if layout >= 0 else
-                       "k_gather<16, TableSrc> (P2PCacheFeatureServer gather, address table)"),
+                       "k_gather<16, U, TableSrc> (P2PCacheFeatureServer gather, address table)") +
+                      "; U = 16-B chunks per lane: 8 for launches of >= 2^21 chunks, else 4",
             "timing": ("device-side s_memrealtime stamps per workgroup (first workgroup start to "
                        "last workgroup end of each launch, 100 MHz wall clock) over the timed "
                        "region, where each gather shares the GPU with the sampling kernels of the "

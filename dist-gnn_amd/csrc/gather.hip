@@ -148,6 +148,13 @@ struct StridedSrc {
 #endif
 constexpr int kGatherThreads = DGS_GATHER_THREADS;
 constexpr int kGatherUnroll = DGS_GATHER_UNROLL;
+// Large 16-byte-chunk gathers take 8 chunks per lane (half the workgroups to dispatch: inside
+// the pipeline the gather's span is mostly the dispatch of its one-wave workgroups).  Round 5,
+// same box, 5 rounds: products-like uniform (3.2 M chunks per launch) gather 0.441 -> 0.455 of
+// 8 TB/s, +0.5 % pipelined; the small biased gathers (0.3-0.9 M chunks) lose with 8 (0.223 ->
+// 0.211) and keep 4 (profiles/r05_ab_gather_unroll.txt).
+constexpr int kGatherUnrollBig = 8;
+constexpr int64_t kGatherBigChunks = int64_t(2) << 20;
 
 // Stores the first out-of-range id a launch met into the process's async error words
 // (context.h): id, row count and call tag first, then the kind with a system-scope release.
@@ -159,7 +166,7 @@ __device__ __attribute__((noinline)) void report_bad_id(int64_t *err, int64_t ki
   __hip_atomic_store(err, kind, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <int V, typename Src>
+template <int V, int U, typename Src>
 __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nchunks,
                                                            uint32_t cpr, FastDivU32 fd,
                                                            char *__restrict__ out,
@@ -190,42 +197,42 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather(Src src, uint32_t nch
   }
   // profiling only (stamp != nullptr, a kernel argument: uniform branch)
   if (stamp && threadIdx.x == 0) stamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-  const uint32_t base = blockIdx.x * (uint32_t)(kGatherThreads * kGatherUnroll) + threadIdx.x;
+  const uint32_t base = blockIdx.x * (uint32_t)(kGatherThreads * U) + threadIdx.x;
   // Branch-free: out-of-range chunks re-read the last chunk and skip only the store, so the
   // U independent id -> address -> row load chains issue back to back (3 waits, not 3U).
-  uint32_t r[kGatherUnroll], c[kGatherUnroll];
-  typename Src::Key key[kGatherUnroll];
-  const char *a[kGatherUnroll];
-  T v[kGatherUnroll];
+  uint32_t r[U], c[U];
+  typename Src::Key key[U];
+  const char *a[U];
+  T v[U];
 #pragma unroll
-  for (int u = 0; u < kGatherUnroll; ++u) {
+  for (int u = 0; u < U; ++u) {
     uint32_t g = base + u * kGatherThreads;
     g = g < nchunks ? g : nchunks - 1;
     r[u] = fd.div(g);
     c[u] = g - r[u] * cpr;
   }
 #pragma unroll
-  for (int u = 0; u < kGatherUnroll; ++u) key[u] = src.key(r[u]);
+  for (int u = 0; u < U; ++u) key[u] = src.key(r[u]);
   // Range guard (one unsigned compare per id): an id outside [0, nrows) would address memory
   // outside the source (a GPU fault); it reads row 0 instead and the launch reports it.
   bool bad = false;
   int64_t bad_id = 0;
 #pragma unroll
-  for (int u = 0; u < kGatherUnroll; ++u) {
+  for (int u = 0; u < U; ++u) {
     const bool b = (uint64_t)key[u] >= gd.nrows;
     bad_id = b ? (int64_t)key[u] : bad_id;
     bad |= b;
     key[u] = b ? 0 : key[u];
   }
 #pragma unroll
-  for (int u = 0; u < kGatherUnroll; ++u) a[u] = src.addr(key[u]);
+  for (int u = 0; u < U; ++u) a[u] = src.addr(key[u]);
 #pragma unroll
-  for (int u = 0; u < kGatherUnroll; ++u)
+  for (int u = 0; u < U; ++u)
     v[u] = *to_global<T>(a[u] + (size_t)c[u] * V);
 #pragma unroll
-  for (int u = 0; u < kGatherUnroll; ++u) keep(v[u]);
+  for (int u = 0; u < U; ++u) keep(v[u]);
 #pragma unroll
-  for (int u = 0; u < kGatherUnroll; ++u) {
+  for (int u = 0; u < U; ++u) {
     const uint32_t g = base + u * kGatherThreads;
     // non-temporal: the output is consumed by the next kernel, not re-read here, so it
     // streams past L2 instead of evicting the rows other waves are fetching
@@ -244,14 +251,16 @@ void launch_gather_v(int V, Src src, int64_t n, int64_t row_bytes, char *out, hi
                      int which, GatherGuard gd, const LabelTail *tail = nullptr) {
   const int64_t cpr = row_bytes / V;
   DGS_CHECK(cpr > 0 && cpr < (int64_t(1) << 30), "gather: unsupported row size");
-  const int64_t max_rows = ((int64_t(1) << 31) - kGatherThreads * kGatherUnroll) / cpr;
+  const int64_t max_rows = ((int64_t(1) << 31) - kGatherThreads * kGatherUnrollBig) / cpr;
   const FastDivU32 fd = FastDivU32::make((uint32_t)cpr);
   for (int64_t r0 = 0; r0 < n; r0 += max_rows) {
     const int64_t rows = n - r0 < max_rows ? n - r0 : max_rows;
     Src s = src;
     s.row_base = r0;
     const uint32_t nchunks = (uint32_t)(rows * cpr);
-    dim3 grid((unsigned)ceil_div(nchunks, kGatherThreads * kGatherUnroll));
+    const bool big = V == 16 && (int64_t)nchunks >= kGatherBigChunks;
+    const int U = big ? kGatherUnrollBig : kGatherUnroll;
+    dim3 grid((unsigned)ceil_div(nchunks, kGatherThreads * U));
     char *o = out + r0 * row_bytes;
     // stamps cover the feature workgroups only (the label workgroups return before stamping)
     uint64_t *stamp = profile_stamps(which, (int64_t)grid.x);
@@ -263,12 +272,18 @@ void launch_gather_v(int V, Src src, int64_t n, int64_t row_bytes, char *out, hi
     }
     const dim3 block(kGatherThreads);
     const uint32_t c32 = (uint32_t)cpr;
+    constexpr int U4 = kGatherUnroll, U8 = kGatherUnrollBig;
     switch (V) {
-      case 16: hipLaunchKernelGGL((k_gather<16, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
-      case 8: hipLaunchKernelGGL((k_gather<8, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
-      case 4: hipLaunchKernelGGL((k_gather<4, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
-      case 2: hipLaunchKernelGGL((k_gather<2, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
-      default: hipLaunchKernelGGL((k_gather<1, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
+      case 16:
+        if (big)
+          hipLaunchKernelGGL((k_gather<16, U8, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd);
+        else
+          hipLaunchKernelGGL((k_gather<16, U4, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd);
+        break;
+      case 8: hipLaunchKernelGGL((k_gather<8, U4, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
+      case 4: hipLaunchKernelGGL((k_gather<4, U4, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
+      case 2: hipLaunchKernelGGL((k_gather<2, U4, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
+      default: hipLaunchKernelGGL((k_gather<1, U4, Src>), grid, block, 0, st, s, nchunks, c32, fd, o, stamp, lt, gd); break;
     }
     DGS_LAUNCH_CHECK();
   }

@@ -14,6 +14,14 @@ import os
 import sys
 
 
+def unroll_of(name):
+    """16-B chunks per lane of a gather launch: the kernel's second template argument since
+    round 5 (k_gather<16, 8, ...> for large gathers), 4 before."""
+    import re
+    m = re.search(r"k_gather<16, (\d+), ", name)
+    return int(m.group(1)) if m else 4
+
+
 def per_kernel(path_glob, counter, kernel_re, with_grid=False):
     import re
     vals = []
@@ -21,16 +29,19 @@ def per_kernel(path_glob, counter, kernel_re, with_grid=False):
         for r in csv.DictReader(open(path)):
             if r.get("Counter_Name") != counter:
                 continue
-            if re.search(kernel_re, r.get("Kernel_Name", "")):
+            name = r.get("Kernel_Name", "")
+            if re.search(kernel_re, name):
                 v = float(r["Counter_Value"])
-                vals.append((v, int(r.get("Grid_Size", 0) or 0)) if with_grid else v)
+                vals.append((v, int(r.get("Grid_Size", 0) or 0) * unroll_of(name))
+                            if with_grid else v)
     return vals
 
 
-def rows_of_grid(grid_threads, row_bytes, vec=16, threads=64, unroll=4):
-    """Rows of one gather launch from its grid (one-wave workgroups, `unroll` 16-B chunks per
-    lane; the fused label workgroups, at most a few dozen, are within the rounding)."""
-    return max(1.0, grid_threads / threads * threads * unroll / (row_bytes / vec))
+def rows_of_grid(grid_chunks_per_lane, row_bytes, vec=16, threads=64):
+    """Rows of one gather launch from its grid size times the launch's chunks per lane
+    (one-wave workgroups; the fused label workgroups, at most a few dozen, are within the
+    rounding)."""
+    return max(1.0, grid_chunks_per_lane / (row_bytes / vec))
 
 
 def bench_side(fetch, write, row_bytes):
@@ -55,8 +66,9 @@ def kernel_names(path_glob):
 def main(root):
     # the feature-server gather: computed addresses (StridedSrc, whole graph cached) or the
     # address-table form (TableSrc)
-    table_re = r"k_gather<16, dgs::\(anonymous namespace\)::(TableSrc|StridedSrc<\w+>) ?>"
-    plain_re = r"k_gather<16, dgs::\(anonymous namespace\)::PlainSrc<long> >"
+    table_re = (r"k_gather<16, (\d+, )?dgs::\(anonymous namespace\)::"
+                r"(TableSrc|StridedSrc<\w+>) ?>")
+    plain_re = r"k_gather<16, (\d+, )?dgs::\(anonymous namespace\)::PlainSrc<long> >"
     bf = per_kernel(f"{root}/pmc_bench_fetch/**/*counter_collection.csv", "FETCH_SIZE", table_re,
                     with_grid=True)
     bw = per_kernel(f"{root}/pmc_bench_write/**/*counter_collection.csv", "WRITE_SIZE", table_re,
