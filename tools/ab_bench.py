@@ -3,7 +3,8 @@ given variants and prints the median ms/step, sample span and gather roofline of
 noise is about 3 %, so kernel changes worth 1-2 % are only visible side by side.
 
 A variant is a libdgs_amd.so path (DGS_AMD_LIB), optionally followed by comma-separated
-environment settings: `ab/u8/libdgs_amd.so,DGS_HUB_BLOCKS=1024`.
+environment settings: `ab/u8/libdgs_amd.so,DGS_HUB_BLOCKS=1024`; a setting that starts with
+`--` is a bench argument instead (`ab/u8/libdgs_amd.so,--depth=4,GPU_MAX_HW_QUEUES=8`).
 
     python tools/ab_bench.py --rounds 3 -- ab/a/libdgs_amd.so ab/b/libdgs_amd.so [-- bench args]
 """
@@ -20,9 +21,15 @@ def variant_env(spec):
     parts = spec.split(",")
     env = dict(os.environ, DGS_AMD_LIB=os.path.abspath(parts[0]))
     for kv in parts[1:]:
+        if kv.startswith("--"):
+            continue
         k, v = kv.split("=", 1)
         env[k] = v
     return env
+
+
+def variant_args(spec):
+    return [kv for kv in spec.split(",")[1:] if kv.startswith("--")]
 
 
 def main():
@@ -40,7 +47,7 @@ def main():
     res = {lib: [] for lib in libs}
     for r in range(rounds):
         for lib in libs:
-            cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline"] + extra
+            cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline"] + extra + variant_args(lib)
             if "--secondary" not in extra:
                 cmd += ["--secondary", "none"]
             out = subprocess.run(cmd, env=variant_env(lib), capture_output=True, text=True,
