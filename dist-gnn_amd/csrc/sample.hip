@@ -62,6 +62,23 @@ int bias_stream_blocks() {
   return n;
 }
 
+// Upper bounds on the biased boot / merge grids (the hop's S bounds both); DGS_BIAS_BOOT_BLOCKS /
+// DGS_BIAS_MERGE_BLOCKS override (round 5 A/B, papers-like: 4096 / 2048 at the plateau,
+// profiles/r05_ab_bias_boot_merge_grid.txt).
+int env_blocks(const char *name, int dflt) {
+  const char *e = getenv(name);
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : dflt;
+}
+int bias_boot_blocks() {
+  static const int n = env_blocks("DGS_BIAS_BOOT_BLOCKS", 4096);
+  return n;
+}
+int bias_merge_blocks() {
+  static const int n = env_blocks("DGS_BIAS_MERGE_BLOCKS", 2048);
+  return n;
+}
+
 using RowInfo = NodeEntry;  // {absolute neighbour-id pointer, degree | location << 56}
 
 __device__ __forceinline__ int64_t ri_deg(const RowInfo &r) { return r.dl & kOffMask; }
@@ -1804,8 +1821,8 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     if (bias_hubs) {
       ba = BiasHubArgs{src,  Sc,     k,   launch_seed, rowinfo, tpre, boff,
                        hub,  nworkers, rowpos, col, table,   cand};
-      hipLaunchKernelGGL(k_bias_boot, dim3((unsigned)std::min<int64_t>(S, 4096)), dim3(kTileRows),
-                         0, st, ba);
+      hipLaunchKernelGGL(k_bias_boot, dim3((unsigned)std::min<int64_t>(S, bias_boot_blocks())),
+                         dim3(kTileRows), 0, st, ba);
       DGS_LAUNCH_CHECK();
       // DGS_BIAS_STATS=1 (diagnostics, synchronises): the hop's hub rows and their edges
       static const bool stats = getenv("DGS_BIAS_STATS") != nullptr;
@@ -1877,13 +1894,14 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
                            launch_seed, rowinfo, tpre, boff, tpre2, tboff, cdf, rowpos, col,
                            table, (const int64_t *)hub.hubid);
         DGS_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_bias_hub_merge, dim3((unsigned)std::min<int64_t>(S, 2048)),
+        hipLaunchKernelGGL(k_bias_hub_merge,
+                           dim3((unsigned)std::min<int64_t>(S, bias_merge_blocks())),
                            dim3(kTileRows), 0, st, ba);
         DGS_LAUNCH_CHECK();
         return;
       }
       if (bias_hubs) {
-        const int64_t mb = std::min<int64_t>(S, 2048);
+        const int64_t mb = std::min<int64_t>(S, bias_merge_blocks());
         hipLaunchKernelGGL(k_bias_rows_merge, dim3((unsigned)(grid.x + mb)), dim3(kTileRows), 0,
                            st, ba, (const int32_t *)tpre2, (const int64_t *)tboff,
                            (int64_t)grid.x, mb);
