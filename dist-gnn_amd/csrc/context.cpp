@@ -348,6 +348,7 @@ struct StampRec {
   int64_t nblocks;
   int which;
   bool own;  // a separate allocation (slab full), returned to the pool at collect
+  int extra;  // words per workgroup after the 2 x nblocks stamps (kernel-defined counters)
 };
 // Workgroup stamps are bump-allocated from one slab reserved when profiling is switched on,
 // so a profiled launch inside a timed region never calls hipMalloc.  1 GiB holds 2 x 8 B for
@@ -401,27 +402,28 @@ KernelEvents profile_kernel(int which) {
   return ev;
 }
 
-uint64_t *profile_stamps(int which, int64_t nblocks) {
+uint64_t *profile_stamps(int which, int64_t nblocks, int extra) {
   if (!profiler().wants(which) || nblocks <= 0) return nullptr;
   std::lock_guard<std::mutex> g(prof_mu());
   uint64_t *buf = nullptr;
+  const int64_t words = (2 + extra) * nblocks;
   StampSlab &slab = stamp_slab();
-  if (slab.base && slab.used + 2 * nblocks <= kStampSlabWords) {
+  if (slab.base && slab.used + words <= kStampSlabWords) {
     buf = slab.base + slab.used;
-    slab.used += 2 * nblocks;
-    stamp_recs().push_back(StampRec{buf, nblocks, which, false});
+    slab.used += words;
+    stamp_recs().push_back(StampRec{buf, nblocks, which, false, extra});
     return buf;
   }
-  auto &pool = stamp_pool();
+  auto &pool = stamp_pool();  // (capacity in words, buffer)
   for (auto it = pool.begin(); it != pool.end(); ++it) {
-    if (it->first >= nblocks) {
+    if (it->first >= words) {
       buf = it->second;
       pool.erase(it);
       break;
     }
   }
-  if (!buf) DGS_HIP(hipMalloc(reinterpret_cast<void **>(&buf), sizeof(uint64_t) * 2 * nblocks));
-  stamp_recs().push_back(StampRec{buf, nblocks, which, true});
+  if (!buf) DGS_HIP(hipMalloc(reinterpret_cast<void **>(&buf), sizeof(uint64_t) * words));
+  stamp_recs().push_back(StampRec{buf, nblocks, which, true, extra});
   return buf;
 }
 
@@ -471,8 +473,14 @@ void profile_collect() {
     constexpr int kW = 5;
     double d_span[kW] = {}, d_spread[kW] = {}, d_wg[kW] = {}, d_end[kW] = {}, d_busy[kW] = {};
     int64_t d_n[kW] = {};
+    // k_bias_stream's per-workgroup counters (extra == 2: candidate flushes, candidates | row
+    // switches << 32): workgroup duration against each, in buckets (the end-spread question)
+    constexpr int kB = 6;
+    double c_dur[3][kB] = {}, c_n[3][kB] = {};
+    auto bucket = [](uint64_t v) { return v < 4 ? (int)v : (v < 8 ? 4 : 5); };
+    double cu_dur[7] = {}, cu_n[7] = {}, cu_count = 0, cu_launch = 0;
     for (auto &r : sr) {
-      h.resize((size_t)(2 * r.nblocks));
+      h.resize((size_t)((2 + r.extra) * r.nblocks));
       DGS_HIP(hipMemcpy(h.data(), r.buf, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost));
       uint64_t t0 = ~0ull, t1 = 0, s1 = 0, e0 = ~0ull;
       double wg = 0;
@@ -494,7 +502,50 @@ void profile_collect() {
           d_n[r.which] += 1;
         }
       }
-      if (r.own) stamp_pool().push_back({r.nblocks, r.buf});
+      // (launches whose workgroups average over 10 us: the ones with work for every worker)
+      if (detail && r.extra == 2 && khz > 0 && wg / (double)r.nblocks > khz / 100.0) {
+        // the launch's mean workgroup duration, so buckets compare within launches
+        const double mean = wg / (double)r.nblocks;
+        // workgroups of this launch per CU (the upper word of the first counter: CU id)
+        std::map<uint64_t, int> per_cu;
+        for (int64_t b = 0; b < r.nblocks; ++b) per_cu[h[2 * r.nblocks + 2 * b] >> 32] += 1;
+        for (int64_t b = 0; b < r.nblocks; ++b) {
+          const int share = per_cu[h[2 * r.nblocks + 2 * b] >> 32];
+          const int sb = share < 6 ? share : 6;
+          cu_dur[sb] += (double)(h[2 * b + 1] - h[2 * b]) / mean;
+          cu_n[sb] += 1;
+        }
+        cu_count += (double)per_cu.size();
+        cu_launch += 1;
+        for (int64_t b = 0; b < r.nblocks; ++b) {
+          const double dur = (double)(h[2 * b + 1] - h[2 * b]) / mean;
+          const uint64_t fl = h[2 * r.nblocks + 2 * b] & 0xffffffffu;
+          const uint64_t cr = h[2 * r.nblocks + 2 * b + 1];
+          const uint64_t v[3] = {fl, (cr & 0xffffffffu) / 64, cr >> 32};
+          for (int j = 0; j < 3; ++j) {
+            c_dur[j][bucket(v[j])] += dur;
+            c_n[j][bucket(v[j])] += 1;
+          }
+        }
+      }
+      if (r.own) stamp_pool().push_back({(2 + r.extra) * r.nblocks, r.buf});
+    }
+    if (detail && cu_launch > 0) {
+      fprintf(stderr, "[dgs prof] k_bias_stream: %.1f CUs per launch; workgroups by launch "
+              "workgroups on their CU (1..5, 6+): duration / launch mean", cu_count / cu_launch);
+      for (int sb = 1; sb < 7; ++sb)
+        fprintf(stderr, " %.3f (n %.0f)", cu_n[sb] ? cu_dur[sb] / cu_n[sb] : 0.0, cu_n[sb]);
+      fprintf(stderr, "\n");
+    }
+    static const char *cname[3] = {"candidate flushes", "candidates / 64", "row switches"};
+    for (int j = 0; detail && j < 3; ++j) {
+      if (c_n[j][0] + c_n[j][1] + c_n[j][2] + c_n[j][3] + c_n[j][4] + c_n[j][5] == 0) continue;
+      fprintf(stderr, "[dgs prof] k_bias_stream workgroups by %s (0,1,2,3,4-7,8+): "
+              "duration / launch mean", cname[j]);
+      for (int bk = 0; bk < kB; ++bk)
+        fprintf(stderr, " %.3f (n %.0f)", c_n[j][bk] ? c_dur[j][bk] / c_n[j][bk] : 0.0,
+                c_n[j][bk]);
+      fprintf(stderr, "\n");
     }
     for (int w = 0; detail && w < kW; ++w)
       if (d_n[w])

@@ -184,7 +184,8 @@ KernelEvents profile_kernel(int which);
 // after its last store (the launch's duration = last end - first start, the kernel's own
 // execution span); nullptr otherwise.  Unlike stream events it excludes the tail of the
 // previous kernel on the stream and any wait for free CUs before the first workgroup starts.
-uint64_t *profile_stamps(int which, int64_t nblocks);
+// (extra: counter words per workgroup after the 2 x nblocks stamps)
+uint64_t *profile_stamps(int which, int64_t nblocks, int extra = 0);
 // Stream events at both ends of a group of launches (one marker before the first and one
 // after the last kernel; used around a whole sample call, where the stream is idle anyway,
 // never between the kernels being measured).

@@ -1055,7 +1055,9 @@ __device__ __forceinline__ void merge_emit(const BiasHubArgs &a, int64_t S, int6
   const RowInfo ri = a.rowinfo[r];
   const int64_t out = a.boff[r / kTileRows] + a.tpre[r];
   if (l < k) {
-    const int64_t v = as_global(ri.ptr)[idx_l];
+    // (a pick outside the row -- only if the filter's proven bound failed -- emits id -1,
+    // which the relabel tail reports, instead of reading outside the row)
+    const int64_t v = (uint32_t)idx_l < (uint64_t)ri_deg(ri) ? as_global(ri.ptr)[idx_l] : -1;
     a.rowpos[out + l] = r;
     a.col[out + l] = v;
     table_record(a.table, v, S + out + l);
@@ -1346,8 +1348,17 @@ __global__ __launch_bounds__(kTileRows) void k_bias_boot(BiasHubArgs a) {
 // does the hop's tile-offset scan (the rows / merge launch after it reads boff).  Row state is
 // kept in 32 bits (a row has < 2^31 edges, a lane's draw offset < 2^28, the hop's chunk count
 // and candidate room < 2^31): register pressure, not arithmetic, sets this kernel's occupancy.
+// DGS_STREAM_COUNTERS (diagnostic builds only): per half-wave candidate flushes, candidates
+// and row switches, summed per workgroup into the profiling stamps (DGS_PROF_HUB=1).
+#ifndef DGS_STREAM_COUNTERS
+#define DGS_STREAM_COUNTERS 0
+#endif
+struct StreamCounters {
+  uint32_t flushes = 0, cands = 0, switches = 0;
+};
 __device__ __forceinline__ void bias_stream_body(const BiasHubArgs &a, const int64_t *bsum,
-                                                 int64_t *boff, int64_t *d_nnz) {
+                                                 int64_t *boff, int64_t *d_nnz,
+                                                 StreamCounters &sc) {
   if (blockIdx.x == 0) {
     __shared__ int64_t lds[kTileRows / 64];
     const int64_t nb = (a.Sc.get() + kTileRows - 1) / kTileRows;
@@ -1463,6 +1474,10 @@ __device__ __forceinline__ void bias_stream_body(const BiasHubArgs &a, const int
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (DGS_STREAM_COUNTERS) {
+      sc.flushes += 1;
+      sc.cands += (uint32_t)nb;
+    }
     nb = 0;
   };
   load_row(h);
@@ -1473,6 +1488,7 @@ __device__ __forceinline__ void bias_stream_body(const BiasHubArgs &a, const int
     while (ch >= hnext) {
       ++h;
       load_row(h);
+      if (DGS_STREAM_COUNTERS) sc.switches += 1;
     }
     if (skip) continue;
     const uint32_t q = ch - hstart;
@@ -1532,11 +1548,32 @@ __global__ __launch_bounds__(kTileRows) void k_bias_stream(BiasHubArgs a, const 
                                                            uint64_t *stamp) {
   // profiling only (DGS_PROF_HUB: stamp != nullptr, a kernel argument: uniform branch)
   if (stamp && threadIdx.x == 0) stamp[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-  bias_stream_body(a, bsum, boff, d_nnz);
+  __shared__ uint32_t s_ctr[3];
+  if (DGS_STREAM_COUNTERS && stamp) {
+    if (threadIdx.x < 3) s_ctr[threadIdx.x] = 0;
+    __syncthreads();
+  }
+  StreamCounters sc;
+  bias_stream_body(a, bsum, boff, d_nnz, sc);
   if (stamp) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (DGS_STREAM_COUNTERS && (threadIdx.x & 31) == 0) {
+      atomicAdd(&s_ctr[0], sc.flushes);
+      atomicAdd(&s_ctr[1], sc.cands);
+      atomicAdd(&s_ctr[2], sc.switches);
+    }
     __syncthreads();
-    if (threadIdx.x == 0) stamp[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+      stamp[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+      if (DGS_STREAM_COUNTERS) {
+        uint64_t *ctr = stamp + 2 * gridDim.x + 2 * blockIdx.x;
+        // the workgroup's CU: HW_ID bits 8-15 (CU, SH, SE) and the XCC id
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+        ctr[0] = (uint64_t)s_ctr[0] | ((uint64_t)(((hw >> 8) & 0xff) | ((xcc & 0xff) << 8)) << 32);
+        ctr[1] = (uint64_t)s_ctr[1] | ((uint64_t)s_ctr[2] << 32);
+      }
+    }
   }
 }
 
@@ -1553,7 +1590,7 @@ __device__ __forceinline__ void merge_emit_at(const BiasHubArgs &a, int64_t S, i
                                               const RowInfo &ri, int64_t out, int32_t idx_l,
                                               int64_t k, int l) {
   if (l < k) {
-    const int64_t v = as_global(ri.ptr)[idx_l];
+    const int64_t v = (uint32_t)idx_l < (uint64_t)ri_deg(ri) ? as_global(ri.ptr)[idx_l] : -1;
     a.rowpos[out + l] = r;
     a.col[out + l] = v;
     table_record(a.table, v, S + out + l);
@@ -1848,7 +1885,7 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
       // (its workgroup 0 also does the hop's tile-offset scan)
       hipLaunchKernelGGL(k_bias_stream, dim3(bias_stream_blocks()), dim3(kTileRows), 0, st, ba,
                          (const int64_t *)bsum, boff, d_nnz,
-                         profile_stamps(4, bias_stream_blocks()));
+                         profile_stamps(4, bias_stream_blocks(), DGS_STREAM_COUNTERS ? 2 : 0));
       DGS_LAUNCH_CHECK();
       if (stats) {  // candidates per hub row after the stream
         DGS_HIP(hipStreamSynchronize(st));
