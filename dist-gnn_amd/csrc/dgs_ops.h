@@ -125,7 +125,7 @@ struct HopScratch {
 void sample_hop(const RowSrc &src, const int64_t *seeds, Count S, int64_t k, bool replace,
                 bool bias, uint64_t launch_seed, int64_t *rowpos, int64_t *col, int64_t *d_nnz,
                 const Table &table, HopScratch &ws, hipStream_t st,
-                const RelabelTail *tail = nullptr);
+                const RelabelTail *tail = nullptr, bool solo = false);
 
 // Test-only: exact A-Res keys, their lower bounds and the biased kernels' reject tests.
 void test_bias_bounds(const uint32_t *x, const float *p, const float *thr, int64_t n, float *key,

@@ -279,7 +279,8 @@ void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_o
                      int64_t *const *cols, int64_t *sizes, hipStream_t st,
                      const uint64_t *launch_seeds) {
   if (L <= 0) return;
-  sample_begin(seeds, n_seeds, fan_out, L, replace, frontiers, rows, cols, st, launch_seeds);
+  sample_begin(seeds, n_seeds, fan_out, L, replace, frontiers, rows, cols, st, launch_seeds,
+               /*host_async=*/false, /*solo=*/true);
   sample_end(L, sizes, st);
 }
 
@@ -295,7 +296,7 @@ constexpr int kSizes0 = kFlagWord + 1;
 void Sampler::sample_begin(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_out,
                            int L, bool replace, int64_t *const *frontiers,
                            int64_t *const *rows, int64_t *const *cols, hipStream_t st,
-                           const uint64_t *launch_seeds, bool host_async) {
+                           const uint64_t *launch_seeds, bool host_async, bool solo) {
   DGS_CHECK(L > 0, "sample: empty fan_out");
   for (int h = 0; h < L; ++h) DGS_CHECK(fan_out[h] >= 0, "fan_out entries must be non-negative");
   Job j;
@@ -303,6 +304,7 @@ void Sampler::sample_begin(const int64_t *seeds, int64_t n_seeds, const int64_t 
   j.n_seeds = n_seeds;
   j.L = L;
   j.replace = replace;
+  j.solo = solo;
   j.fan_out.assign(fan_out, fan_out + L);
   j.fr.assign(frontiers, frontiers + L);
   j.rows.assign(rows, rows + L);
@@ -469,7 +471,7 @@ void Sampler::launch_hops(Ctx &c, const Job &j, hipStream_t st) {
     c.dirty[tb] = true;
     // rows[h] receives each edge's seed row r from the sampler and is relabelled in place
     sample_hop(src, cur, S, k, replace, bias_, seed, rows[h], cols[h], d_nnz, t, c.ws, st,
-               have_tail ? &tail : nullptr);
+               have_tail ? &tail : nullptr, j.solo);
     if (have_tail) c.dirty[tb ^ 1] = false;  // the previous hop's clean-up is enqueued
     // the last hop's scatter publishes the flag word and every size to pinned host memory (no
     // copy, no sync); each hop's count pass range-checks its sampled ids before that, so the

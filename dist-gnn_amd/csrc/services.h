@@ -76,7 +76,7 @@ class Sampler {
   void sample_begin(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_out, int L,
                     bool replace, int64_t *const *frontiers, int64_t *const *rows,
                     int64_t *const *cols, hipStream_t st, const uint64_t *launch_seeds,
-                    bool host_async = false);
+                    bool host_async = false, bool solo = false);
   void sample_end(int L, int64_t *sizes, hipStream_t st);
   // `consumer` waits for the last call ended on `st`, on the event that call recorded after its
   // launches (no event record on the caller's thread).
@@ -113,6 +113,7 @@ class Sampler {
     std::vector<int64_t> fan_out;
     std::vector<int64_t *> fr, rows, cols;
     std::vector<uint64_t> hop_seed;
+    bool solo = false;  // a synchronous call (sample()): nothing else of ours runs beside it
   };
   struct Ctx {
     std::mutex mu;
