@@ -27,7 +27,10 @@ namespace dgs {
 namespace {
 
 constexpr int kTileRows = 256;   // rows per prep / sample workgroup
-constexpr int kGroup = 16;       // lanes per row in the uniform kernel
+#ifndef DGS_UNIFORM_GROUP
+#define DGS_UNIFORM_GROUP 16
+#endif
+constexpr int kGroup = DGS_UNIFORM_GROUP;  // lanes per row in the uniform kernel
 constexpr int kRowsPerBlock = kTileRows / kGroup;  // rows per uniform-sampling workgroup
 constexpr int kHubT = 128;       // reservoir tail length above which a row goes to the hub kernel
 #ifndef DGS_BIAS_HUB_T
