@@ -27,11 +27,12 @@ namespace dgs {
 namespace {
 
 constexpr int kTileRows = 256;   // rows per prep / sample workgroup
-#ifndef DGS_UNIFORM_GROUP
-#define DGS_UNIFORM_GROUP 16
-#endif
-constexpr int kGroup = DGS_UNIFORM_GROUP;  // lanes per row in the uniform kernel
-constexpr int kRowsPerBlock = kTileRows / kGroup;  // rows per uniform-sampling workgroup
+// Lanes per row in the uniform row kernel (rows per workgroup = kTileRows / lanes).  Round 5
+// A/B (profiles/r05_ab_uniform_row_group.txt): wider groups shorten one call's chain (sample
+// span 171.6 -> 165.7 us with 64 lanes) but cost the 3-deep pipeline 2-3 %, narrower ones lose
+// both ways -- synchronous calls use kGroupSolo, a loader's calls kGroup.
+constexpr int kGroup = 16;
+constexpr int kGroupSolo = 64;
 constexpr int kHubT = 128;       // reservoir tail length above which a row goes to the hub kernel
 #ifndef DGS_BIAS_HUB_T
 #define DGS_BIAS_HUB_T 1024
@@ -379,10 +380,11 @@ __device__ __forceinline__ int64_t nb_load(global_ptr<int64_t> nb, int64_t i) {
 }
 
 // Writes the k picks of row r whose reservoir slots are `slots` (16-lane group, lane L).
+template <int G>
 __device__ __forceinline__ void emit_slots(const UniformArgs &a, int64_t S, int64_t r,
                                            global_ptr<int64_t> nb, int64_t out,
                                            const int32_t *slots, int L) {
-  for (int64_t s2 = L; s2 < a.k; s2 += kGroup) {
+  for (int64_t s2 = L; s2 < a.k; s2 += G) {
     const int64_t v = nb_load(nb, slots[s2]);
     a.rowpos[out + s2] = r;
     a.col[out + s2] = v;
@@ -510,13 +512,13 @@ __device__ __forceinline__ void hub_reservoir(const UniformArgs &a, int64_t gw, 
 
 // Rows of one 16-row block, a 16-lane group per row.  A hub row (hubid >= 0) takes its k picks
 // from the global slots k_hub_reservoir filled.
-template <bool kReplace>
+template <bool kReplace, int G>
 __device__ __forceinline__ void sample_rows(const UniformArgs &a, int64_t blk, int32_t *s_slot,
                                             bool use_hubs) {
   const int64_t S = a.Sc.get();
   const int64_t k = a.k;
-  const int g = threadIdx.x / kGroup, L = threadIdx.x % kGroup;
-  const int64_t r = blk * kRowsPerBlock + g;
+  const int g = threadIdx.x / G, L = threadIdx.x % G;
+  const int64_t r = blk * (kTileRows / G) + g;
   if (r >= S) return;
   int32_t *sl = s_slot + g * k;
   const RowInfo ri = a.rowinfo[r];
@@ -527,7 +529,7 @@ __device__ __forceinline__ void sample_rows(const UniformArgs &a, int64_t blk, i
   const uint2 kk = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
   if (kReplace) {
     if (deg > 0) {
-      for (int64_t p = L; p < k; p += kGroup) {
+      for (int64_t p = L; p < k; p += G) {
         const int64_t t = p & 127, j = p >> 7;
         const uint4 o4 = philox4x32_10(make_uint4((uint32_t)(j >> 2), 0u, (uint32_t)t, 0u), kk);
         const uint32_t x = u4_get(o4, (int)(j & 3));
@@ -541,7 +543,7 @@ __device__ __forceinline__ void sample_rows(const UniformArgs &a, int64_t blk, i
     return;
   }
   if (deg <= k) {
-    for (int64_t p = L; p < deg; p += kGroup) {
+    for (int64_t p = L; p < deg; p += G) {
       const int64_t v = nb_load(nb, p);
       a.rowpos[out + p] = r;
       a.col[out + p] = v;
@@ -552,15 +554,15 @@ __device__ __forceinline__ void sample_rows(const UniformArgs &a, int64_t blk, i
   // a hub row (prep's test, from the degree alone: no hub-index load) takes the slots
   // k_hub_reservoir filled; they are indexed by row
   if (use_hubs && deg - k > kHubT) {
-    emit_slots(a, S, r, nb, out, a.hubslot + r * k, L);
+    emit_slots<G>(a, S, r, nb, out, a.hubslot + r * k, L);
     return;
   }
-  for (int64_t s2 = L; s2 < k; s2 += kGroup) sl[s2] = (int32_t)s2;
+  for (int64_t s2 = L; s2 < k; s2 += G) sl[s2] = (int32_t)s2;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   for (int64_t q = 0; k + 512 * q < deg; ++q) {
-    for (int tt = 0; tt < 128 / kGroup; ++tt) {
-      const int t = L + kGroup * tt;
+    for (int tt = 0; tt < 128 / G; ++tt) {
+      const int t = L + G * tt;
       const int64_t base = k + t + 512 * q;
       if (base >= deg) break;
       const uint4 o4 = philox4x32_10(
@@ -579,7 +581,7 @@ __device__ __forceinline__ void sample_rows(const UniformArgs &a, int64_t blk, i
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  emit_slots(a, S, r, nb, out, sl, L);
+  emit_slots<G>(a, S, r, nb, out, sl, L);
 }
 
 // Hub kernel.  Its workgroup 0 first does the hop's tile-offset scan (k_scan_hop's job:
@@ -612,11 +614,11 @@ __global__ __launch_bounds__(256) void k_hub_reservoir(UniformArgs a, const int6
   }
 }
 
-template <bool kReplace>
+template <bool kReplace, int G>
 __global__ __launch_bounds__(kTileRows) void k_sample_uniform(UniformArgs a, int use_hubs) {
   latency_prio();
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  sample_rows<kReplace>(a, blockIdx.x, reinterpret_cast<int32_t *>(smem), use_hubs != 0);
+  sample_rows<kReplace, G>(a, blockIdx.x, reinterpret_cast<int32_t *>(smem), use_hubs != 0);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1862,19 +1864,26 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
     const UniformArgs ua{src,    Sc,  k,     launch_seed, rowinfo,
                          tpre,   boff, hub, ws.hubslot.as<int32_t>(),
                          rowpos, col, table, (int)solo};
-    const size_t lds = replace ? 16 : sizeof(int32_t) * (size_t)kRowsPerBlock * k;
-    const int64_t row_blocks = ceil_div(S, kRowsPerBlock);
+    const int G = solo ? kGroupSolo : kGroup;
+    const int64_t rows_per_block = kTileRows / G;
+    const size_t lds = replace ? 16 : sizeof(int32_t) * (size_t)rows_per_block * k;
+    const int64_t row_blocks = ceil_div(S, rows_per_block);
     if (use_hubs) {
       hipLaunchKernelGGL(k_hub_reservoir, dim3(hub_blocks()), dim3(256), 0, st, ua,
                          (const int64_t *)bsum, boff, d_nnz, profile_stamps(3, hub_blocks()));
       DGS_LAUNCH_CHECK();
     }
-    if (replace)
-      hipLaunchKernelGGL(k_sample_uniform<true>, dim3((unsigned)row_blocks), dim3(kTileRows),
-                         lds, st, ua, 0);
+    const dim3 rgrid((unsigned)row_blocks), rblock(kTileRows);
+    if (replace && solo)
+      hipLaunchKernelGGL((k_sample_uniform<true, kGroupSolo>), rgrid, rblock, lds, st, ua, 0);
+    else if (replace)
+      hipLaunchKernelGGL((k_sample_uniform<true, kGroup>), rgrid, rblock, lds, st, ua, 0);
+    else if (solo)
+      hipLaunchKernelGGL((k_sample_uniform<false, kGroupSolo>), rgrid, rblock, lds, st, ua,
+                         (int)use_hubs);
     else
-      hipLaunchKernelGGL(k_sample_uniform<false>, dim3((unsigned)row_blocks), dim3(kTileRows),
-                         lds, st, ua, (int)use_hubs);
+      hipLaunchKernelGGL((k_sample_uniform<false, kGroup>), rgrid, rblock, lds, st, ua,
+                         (int)use_hubs);
     DGS_LAUNCH_CHECK();
   } else {
     DGS_CHECK(k <= 32, "biased sampling supports num_picks <= 32 (rowwise_sampling_bias.cu:73)");
