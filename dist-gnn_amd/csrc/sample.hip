@@ -56,14 +56,18 @@ int hub_blocks() {
 }
 
 constexpr int kBiasStreamBlocks = 768;  // round 3 A/B: 512-768 best, 1024 -1.5 %, 1536 -9 %
-// Workgroups of the streaming kernel; DGS_BIAS_STREAM_BLOCKS overrides.
-int bias_stream_blocks() {
+// A synchronous call (nothing beside it) prefers more workers: round 4's grid A/B
+// (profiles/r04_ab_bias_stream_grid.txt) had 1024 best for one call (+2-5 %) and 768 for the
+// pipeline.
+constexpr int kBiasStreamBlocksSolo = 1024;
+// Workgroups of the streaming kernel; DGS_BIAS_STREAM_BLOCKS overrides both.
+int bias_stream_blocks(bool solo) {
   static const int n = [] {
     const char *e = getenv("DGS_BIAS_STREAM_BLOCKS");
     const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : kBiasStreamBlocks;
+    return v > 0 ? v : 0;
   }();
-  return n;
+  return n > 0 ? n : (solo ? kBiasStreamBlocksSolo : kBiasStreamBlocks);
 }
 
 // Upper bounds on the biased boot / merge grids (the hop's S bounds both); DGS_BIAS_BOOT_BLOCKS /
@@ -1799,7 +1803,8 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
   // Biased hubs: per-row candidate lists.  Every row's list fits the room below when the graph's
   // edge count is known (a hop's rows are distinct: their chunks number at most E / chunk + S);
   // otherwise rows past it are recomputed exactly.
-  const int64_t nworkers = (int64_t)bias_stream_blocks() * (kTileRows / 32);
+  const int sblocks = bias_stream_blocks(solo);
+  const int64_t nworkers = (int64_t)sblocks * (kTileRows / 32);
   BiasCand cand{};
   if (bias_hubs) {
     // Hub rows have degree > kBiasHubT.  After the first hop the seeds are a frontier (unique
@@ -1918,9 +1923,9 @@ void sample_hop(const RowSrc &src, const int64_t *seeds, Count Sc, int64_t k, bo
                 (long long)((uint64_t)packed & kHubChunkMask));
       }
       // (its workgroup 0 also does the hop's tile-offset scan)
-      hipLaunchKernelGGL(k_bias_stream, dim3(bias_stream_blocks()), dim3(kTileRows), 0, st, ba,
+      hipLaunchKernelGGL(k_bias_stream, dim3(sblocks), dim3(kTileRows), 0, st, ba,
                          (const int64_t *)bsum, boff, d_nnz,
-                         profile_stamps(4, bias_stream_blocks(), DGS_STREAM_COUNTERS ? 2 : 0));
+                         profile_stamps(4, sblocks, DGS_STREAM_COUNTERS ? 2 : 0));
       DGS_LAUNCH_CHECK();
       if (stats) {  // candidates per hub row after the stream
         DGS_HIP(hipStreamSynchronize(st));
