@@ -307,8 +307,13 @@ def timed_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist
         return PrefetchLoader(sampler, seed_batches, fan_out, server=server, labels=labels_dev,
                               depth=args.depth)
 
+    gc_early = os.environ.get("DGS_BENCH_GC_EARLY") == "1"  # (experiment)
+    if gc_early:
+        gc.collect()
+        gc.disable()
     for _ in batches_of([next_seeds() for _ in range(args.warmup)]):
         pass
+    del _
     # the timed batches' seeds (views of the shuffled train set, as SeedGenerator yields them)
     timed = [next_seeds() for _ in range(args.steps)]
     it = batches_of(timed)  # worker threads start here; no batch is submitted before t0
@@ -320,13 +325,21 @@ def timed_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist
     # start / end (no stream markers between the measured kernels)
     if profile:
         dgs.ops.profile_enable(dgs.ops.PROFILE_GATHER)
-    seg0 = torch.cuda.memory_stats(dev).get("segment.all.allocated", 0)
+    # DGS_BENCH_ALLOC_TRACE=1 (diagnostics): the Python stack of every segment the caching
+    # allocator maps inside the timed region, to stderr
+    trace = os.environ.get("DGS_BENCH_ALLOC_TRACE") == "1"
+    if trace:
+        torch.cuda.memory._record_memory_history(max_entries=100000)
+    pools = ("segment.large_pool.allocated", "segment.small_pool.allocated")
+    st0 = torch.cuda.memory_stats(dev)
+    seg0 = [st0.get(k, 0) for k in pools]
     edges = rows = 0
     # Python's cyclic garbage collector is held off inside the timed region: a full collection
     # over torch's object graph stalls the host for milliseconds (a 10 ms step gap was seen in a
     # 1000-step run), which a 20-step run cannot absorb.  No GPU work depends on it.
-    gc.collect()
-    gc.disable()
+    if not gc_early:
+        gc.collect()
+        gc.disable()
     t0 = time.perf_counter()
     step_t = []
     for blocks, x, _ in it:
@@ -341,9 +354,25 @@ def timed_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist
     gc.enable()
     prof = dgs.ops.profile_read() if profile else None
     # hipMalloc calls the caching allocator made inside the timed region (host stalls)
-    mallocs = torch.cuda.memory_stats(dev).get("segment.all.allocated", 0) - seg0
+    st1 = torch.cuda.memory_stats(dev)
+    if trace:
+        snap = torch.cuda.memory._snapshot()
+        torch.cuda.memory._record_memory_history(enabled=None)
+        for dt in snap.get("device_traces", []):
+            for ev in dt:
+                if ev.get("action") == "segment_alloc":
+                    frames = [f"{f['filename']}:{f['line']} {f['name']}"
+                              for f in ev.get("frames", []) if f.get("filename", "").endswith(".py")]
+                    print(f"[bench] segment_alloc {ev.get('size')} B stream {ev.get('stream')}: "
+                          + " <- ".join(frames[:6]), file=sys.stderr)
+    mallocs = {"large_pool": st1.get(pools[0], 0) - seg0[0],
+               "small_pool": st1.get(pools[1], 0) - seg0[1]}
     # host-side spacing of consecutive batches handed out by the loader (jitter diagnostics)
     gaps = np.diff(np.array([t0] + step_t)) * 1e3
+    tr = getattr(it, "trace", None)
+    if tr:  # DGS_PREFETCH_TRACE=1: the first steps' phases, us after t0
+        print("[bench] loader trace: " + " ".join(f"{n}@{(t - t0) * 1e6:.0f}" for n, t in tr[:16]),
+              file=sys.stderr)
     step_gaps = {"p10": float(np.percentile(gaps, 10)), "p50": float(np.median(gaps)),
                  "p90": float(np.percentile(gaps, 90)), "max": float(gaps.max())}
     return elapsed, edges, rows, prof, step_gaps, mallocs

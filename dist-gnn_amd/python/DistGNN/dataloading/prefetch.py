@@ -11,6 +11,7 @@ sampling context per stream over the shared graph.
 import collections
 import os
 import threading
+import time
 
 import torch
 
@@ -35,7 +36,13 @@ _HOST_ASYNC = os.environ.get("DGS_PREFETCH_SYNC", "0") != "1"
 # HIP priority of new batch streams (0 = default; -1 = high: their kernels are dispatched ahead
 # of the default-priority queues')
 _PRIORITY = int(os.environ.get("DGS_PREFETCH_STREAM_PRIORITY", "0"))
+# Ramp-up: batches in flight when the first batch is taken (experiment; 0 = depth)
+_RAMP = int(os.environ.get("DGS_PREFETCH_RAMP", "0"))
+# DGS_PREFETCH_TRACE=1 (diagnostics): host timestamps of each __next__'s phases in self.trace
+_TRACE = os.environ.get("DGS_PREFETCH_TRACE") == "1"
 _STREAMS_LOCK = threading.Lock()
+# (stream, buffer size) pairs whose allocator pool was given a second output buffer
+_PRIMED = set()
 
 
 def _checkout_streams(device, n):
@@ -99,6 +106,8 @@ class PrefetchLoader:
         self._dev = self.device.index
         self._inflight = collections.deque()
         self._n = 0
+        self._taken = 0  # batches handed out
+        self.trace = []
         # seed batches read ahead of their submission, each with the event recorded on the
         # caller's stream when it was read (its batch stream waits on that, not on C's tail)
         self._pulled = collections.deque()
@@ -151,6 +160,16 @@ class PrefetchLoader:
         # int64 seeds (converted on C if need be) + one output buffer from B's pool
         prep = self.sampler._prepare(seeds, self.fan_out, packed=True,
                                      alloc_stream=self._ids[w])
+        key = (st, prep[4])
+        if key not in _PRIMED:
+            # A stream's next call allocates its output while the caller usually still holds
+            # this one (a loop variable lives until the next batch is handed out): the first
+            # time a stream sees this size, a second buffer is allocated and freed at once, so
+            # the caching allocator keeps two blocks in the stream's pool and no later batch
+            # maps a new segment (round 5: the one hipMalloc left inside the bench's timed
+            # region, 27 MB, traced to this allocation).
+            _PRIMED.add(key)
+            self.sampler._prepare(seeds, self.fan_out, packed=True, alloc_stream=self._ids[w])
         # B waits, then the call is enqueued: one C-ABI call.  B is not touched again before
         # result(): the sampler's launcher thread may issue the launches.  The sampler draws
         # the launch seeds once it has accepted the call.
@@ -167,17 +186,27 @@ class PrefetchLoader:
         return self
 
     def __next__(self):
+        if _TRACE:
+            self.trace.append(("next", time.perf_counter()))
         cur = self._caller_stream()
-        while (self._pulled or not self._exhausted) and len(self._inflight) < len(self._st):
+        limit = len(self._st)
+        if _RAMP > 0:  # the k-th batch taken finds at most _RAMP + k batches in flight
+            limit = min(limit, _RAMP + self._taken)
+        while (self._pulled or not self._exhausted) and len(self._inflight) < limit:
             self._submit(cur)
         if not self._inflight:
             self.close()  # returns the streams
             raise StopIteration
         pending, s64, w = self._inflight.popleft()
+        self._taken += 1
         st = self._st[w]
         buf = pending.buffer
+        if _TRACE:
+            self.trace.append(("submitted", time.perf_counter()))
         try:
             blocks = pending.result(cast=False)
+            if _TRACE:
+                self.trace.append(("result", time.perf_counter()))
         except BaseException:
             dgs.ops._stream_wait(st, cur)
             self.close()
@@ -211,6 +240,8 @@ class PrefetchLoader:
                 cast.append((cur_seeds, fr, r, c))
                 cur_seeds = fr
             blocks = cast
+        if _TRACE:
+            self.trace.append(("gathers", time.perf_counter()))
         return blocks, x, y
 
     def close(self):
