@@ -38,6 +38,9 @@ _HOST_ASYNC = os.environ.get("DGS_PREFETCH_SYNC", "0") != "1"
 _PRIORITY = int(os.environ.get("DGS_PREFETCH_STREAM_PRIORITY", "0"))
 # Ramp-up: batches in flight when the first batch is taken (experiment; 0 = depth)
 _RAMP = int(os.environ.get("DGS_PREFETCH_RAMP", "0"))
+# DGS_PREFETCH_RAMP_SYNC=1 (experiment): a loader's first `depth` calls are launched from the
+# caller's thread (its launcher threads may be parked after an idle spell)
+_RAMP_SYNC = os.environ.get("DGS_PREFETCH_RAMP_SYNC") == "1"
 # DGS_PREFETCH_TRACE=1 (diagnostics): host timestamps of each __next__'s phases in self.trace
 _TRACE = os.environ.get("DGS_PREFETCH_TRACE") == "1"
 _STREAMS_LOCK = threading.Lock()
@@ -173,12 +176,13 @@ class PrefetchLoader:
         # B waits, then the call is enqueued: one C-ABI call.  B is not touched again before
         # result(): the sampler's launcher thread may issue the launches.  The sampler draws
         # the launch seeds once it has accepted the call.
+        host_async = _HOST_ASYNC and not (_RAMP_SYNC and self._n <= len(self._st))
         if prep[0] is not seeds:  # converted on C just now: B waits for C's tail
             prep[0].record_stream(self._streams[w])
-            pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, _HOST_ASYNC,
+            pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, host_async,
                                                    st, wait_for=cur)
         else:
-            pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, _HOST_ASYNC,
+            pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, host_async,
                                                    st, wait_event=ev.cuda_event)
         self._inflight.append((pending, prep[0], w))
 
