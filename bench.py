@@ -307,10 +307,15 @@ def timed_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist
         return PrefetchLoader(sampler, seed_batches, fan_out, server=server, labels=labels_dev,
                               depth=args.depth)
 
-    gc_early = os.environ.get("DGS_BENCH_GC_EARLY") == "1"  # (experiment)
-    if gc_early:
-        gc.collect()
-        gc.disable()
+    # Python's cyclic garbage collector is held off from here to the end of the timed region: a
+    # full collection over torch's object graph stalls the host for milliseconds (a 10 ms step
+    # gap was seen in a 1000-step run), which a 20-step run cannot absorb.  It runs once before
+    # the warm-up, not just before t0: a collection walks every Python object and leaves the
+    # host's caches cold, and the first timed submissions then took 250 us instead of 70 us
+    # (round 5, profiles/r05_bench_gc_placement.txt: 20-step value 2.39-2.48 -> 2.72-2.75 G).
+    # No GPU work depends on it.
+    gc.collect()
+    gc.disable()
     for _ in batches_of([next_seeds() for _ in range(args.warmup)]):
         pass
     del _
@@ -334,12 +339,6 @@ def timed_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist
     st0 = torch.cuda.memory_stats(dev)
     seg0 = [st0.get(k, 0) for k in pools]
     edges = rows = 0
-    # Python's cyclic garbage collector is held off inside the timed region: a full collection
-    # over torch's object graph stalls the host for milliseconds (a 10 ms step gap was seen in a
-    # 1000-step run), which a 20-step run cannot absorb.  No GPU work depends on it.
-    if not gc_early:
-        gc.collect()
-        gc.disable()
     t0 = time.perf_counter()
     step_t = []
     for blocks, x, _ in it:
@@ -648,7 +647,8 @@ def run_workload(args, dgs, dist, world, rank, local_rank, mode, share, dev_inde
         # timed region; a mismatch ends the run non-zero on every rank)
         "self_check": self_check,
         "host_step_gap_ms": step_gaps,
-        "python_gc_in_timed_region": "disabled (gc.collect() before, gc.enable() after)",
+        "python_gc_in_timed_region": ("disabled (gc.collect() before the warm-up, gc.enable() "
+                                      "after the timed region)"),
         "allocator_mallocs_in_timed_region": mallocs,
         "host_row_share": side["host_rows"],
         # gathered rows that cached on another GPU (read over xGMI)

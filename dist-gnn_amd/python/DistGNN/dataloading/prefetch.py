@@ -36,11 +36,6 @@ _HOST_ASYNC = os.environ.get("DGS_PREFETCH_SYNC", "0") != "1"
 # HIP priority of new batch streams (0 = default; -1 = high: their kernels are dispatched ahead
 # of the default-priority queues')
 _PRIORITY = int(os.environ.get("DGS_PREFETCH_STREAM_PRIORITY", "0"))
-# Ramp-up: batches in flight when the first batch is taken (experiment; 0 = depth)
-_RAMP = int(os.environ.get("DGS_PREFETCH_RAMP", "0"))
-# DGS_PREFETCH_RAMP_SYNC=1 (experiment): a loader's first `depth` calls are launched from the
-# caller's thread (its launcher threads may be parked after an idle spell)
-_RAMP_SYNC = os.environ.get("DGS_PREFETCH_RAMP_SYNC") == "1"
 # DGS_PREFETCH_TRACE=1 (diagnostics): host timestamps of each __next__'s phases in self.trace
 _TRACE = os.environ.get("DGS_PREFETCH_TRACE") == "1"
 _STREAMS_LOCK = threading.Lock()
@@ -109,7 +104,6 @@ class PrefetchLoader:
         self._dev = self.device.index
         self._inflight = collections.deque()
         self._n = 0
-        self._taken = 0  # batches handed out
         self.trace = []
         # seed batches read ahead of their submission, each with the event recorded on the
         # caller's stream when it was read (its batch stream waits on that, not on C's tail)
@@ -176,13 +170,12 @@ class PrefetchLoader:
         # B waits, then the call is enqueued: one C-ABI call.  B is not touched again before
         # result(): the sampler's launcher thread may issue the launches.  The sampler draws
         # the launch seeds once it has accepted the call.
-        host_async = _HOST_ASYNC and not (_RAMP_SYNC and self._n <= len(self._st))
         if prep[0] is not seeds:  # converted on C just now: B waits for C's tail
             prep[0].record_stream(self._streams[w])
-            pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, host_async,
+            pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, _HOST_ASYNC,
                                                    st, wait_for=cur)
         else:
-            pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, host_async,
+            pending = self.sampler._begin_prepared(seeds, prep, self.replace, None, _HOST_ASYNC,
                                                    st, wait_event=ev.cuda_event)
         self._inflight.append((pending, prep[0], w))
 
@@ -193,16 +186,12 @@ class PrefetchLoader:
         if _TRACE:
             self.trace.append(("next", time.perf_counter()))
         cur = self._caller_stream()
-        limit = len(self._st)
-        if _RAMP > 0:  # the k-th batch taken finds at most _RAMP + k batches in flight
-            limit = min(limit, _RAMP + self._taken)
-        while (self._pulled or not self._exhausted) and len(self._inflight) < limit:
+        while (self._pulled or not self._exhausted) and len(self._inflight) < len(self._st):
             self._submit(cur)
         if not self._inflight:
             self.close()  # returns the streams
             raise StopIteration
         pending, s64, w = self._inflight.popleft()
-        self._taken += 1
         st = self._st[w]
         buf = pending.buffer
         if _TRACE:
