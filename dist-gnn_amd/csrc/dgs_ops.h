@@ -52,6 +52,10 @@ int64_t count_stride_mismatch(const int64_t *list, int64_t n, int64_t start, int
 void ftab_init(int64_t *ftab, int64_t n, const void *base, int64_t row_bytes, hipStream_t st);
 // number of i < n with list[i] outside [0, num_rows) (device count -> host)
 int64_t count_out_of_range(const int64_t *list, int64_t n, int64_t num_rows, hipStream_t st);
+// entries of an address table inside [lo, lo + bytes) / node-table entries at location `loc`
+int64_t count_in_range(const int64_t *tab, int64_t n, const void *lo, int64_t bytes,
+                       hipStream_t st);
+int64_t count_loc(const NodeEntry *tab, int64_t n, int loc, hipStream_t st);
 // ftab[nids[i]] = base + i * row_bytes (ids outside [0, num_rows) are skipped)
 void ftab_assign(int64_t *ftab, int64_t num_rows, const int64_t *nids, int64_t n,
                  const void *base, int64_t row_bytes, hipStream_t st);

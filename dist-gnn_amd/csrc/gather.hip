@@ -396,6 +396,23 @@ __global__ void k_out_of_range(const int64_t *list, int64_t n, int64_t num_rows,
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(bad, c);
 }
 
+// rows of an address table that point into [lo, hi) (a feature table's host rows)
+__global__ void k_count_in_range(const int64_t *tab, int64_t n, uint64_t lo, uint64_t hi,
+                                 unsigned long long *cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = i < n && (uint64_t)tab[i] - lo < hi - lo;
+  const unsigned long long c = __popcll(__ballot(in));
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
+}
+
+// node-table entries whose row lives at location `loc` (a sampler's host rows)
+__global__ void k_count_loc(const NodeEntry *tab, int64_t n, int loc, unsigned long long *cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = i < n && (int)((uint64_t)tab[i].dl >> kLocShift) == loc;
+  const unsigned long long c = __popcll(__ballot(in));
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
+}
+
 template <typename K, typename... A>
 int64_t count_on_device(K kernel, int64_t n, hipStream_t st, A... args) {
   if (n <= 0) return 0;
@@ -421,6 +438,17 @@ int64_t count_stride_mismatch(const int64_t *list, int64_t n, int64_t start, int
 
 int64_t count_out_of_range(const int64_t *list, int64_t n, int64_t num_rows, hipStream_t st) {
   return count_on_device(k_out_of_range, n, st, list, n, num_rows);
+}
+
+int64_t count_in_range(const int64_t *tab, int64_t n, const void *lo, int64_t bytes,
+                       hipStream_t st) {
+  if (!lo || bytes <= 0) return 0;
+  return count_on_device(k_count_in_range, n, st, tab, n, (uint64_t)(uintptr_t)lo,
+                         (uint64_t)(uintptr_t)lo + (uint64_t)bytes);
+}
+
+int64_t count_loc(const NodeEntry *tab, int64_t n, int loc, hipStream_t st) {
+  return count_on_device(k_count_loc, n, st, tab, n, loc);
 }
 
 void ftab_init(int64_t *ftab, int64_t n, const void *base, int64_t row_bytes, hipStream_t st) {

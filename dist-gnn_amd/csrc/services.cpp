@@ -172,6 +172,14 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
     src_.indices_base.p[d] = indices_srv_->ptr(d);
     src_.probs.p[d] = bias_ ? probs_srv_->ptr(d) : nullptr;
   }
+  // Every row cached on some GPU: the host graph was only read to build the caches, so its
+  // registration (pinned, mapped pages: the whole host CSR) is released now instead of being
+  // held for the sampler's life.
+  if (count_loc(ntab, num_nodes, kLocHost, st) == 0) {
+    h_indptr_.detach();
+    h_indices_.detach();
+    h_probs_.detach();
+  }
   src_.indices_base.p[kLocHost] = h_indices_.dev;
   src_.probs.p[kLocHost] = bias_ ? h_probs_.dev : nullptr;
   src_.num_nodes = num_nodes;
@@ -648,6 +656,13 @@ FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_byt
   if (world_ > 1)
     for (void *p : lists) DGS_HIP(hipFree(p));
   DGS_HIP(hipFree(nids));
+  // Every row cached on some GPU: the host matrix was only read to fill the caches; its
+  // registration is released (the alignment test no longer counts the host base).
+  if (count_in_range(ftab, num_rows, h_data_.dev, num_rows * row_bytes, st) == 0) {
+    h_data_.detach();
+    align_or_ = 0;
+    for (int d : rotation(rank_, world_)) align_or_ |= (uintptr_t)feat_srv_->ptr(d);
+  }
 }
 
 // Whole graph cached in a computable layout: the local list is arange(N) (local priority makes

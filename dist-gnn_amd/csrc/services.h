@@ -53,9 +53,13 @@ struct HostView {
     host = p;
     dev = device_view(p, bytes, &registered_here);
   }
-  ~HostView() {
+  // drops this view's registration reference (no device read may follow)
+  void detach() {
     if (registered_here) release_host_view(host);
+    registered_here = false;
+    dev = nullptr;
   }
+  ~HostView() { detach(); }
 };
 
 class Sampler {

@@ -186,3 +186,31 @@ def test_pending_call_of_a_destroyed_sampler_raises(dgs):
     from dgs._lib import lib
     assert lib.dgs_sampler_sample_end(None, 2, None, None) != 0
     assert lib.dgs_feature_server_destroy(None) == 0
+
+
+def test_fully_cached_services_release_the_host_registration(dgs):
+    """A sampler / feature server whose rows are all cached on the GPU reads its host arrays
+    only while it builds the caches: the library's registration of them (pinned, mapped pages)
+    is released at once, and the services stay exact.  A partly cached one keeps it."""
+    from oracle import oracle as O
+    ip, ix = _small_graph(2000, seed=3)
+    n = ip.numel() - 1
+    s_all = dgs.classes.P2PCacheSampler(ip, ix, torch.Tensor(), torch.arange(n), 0)
+    assert not ix.is_pinned() and not ip.is_pinned()
+    seeds = np.random.default_rng(4).permutation(n)[:300]
+    ls = [101, 202, 303]
+    got = s_all._sample_seeded(torch.from_numpy(seeds).cuda(), [15, 10, 5], False, ls)
+    exp = O.node_classification_sample(seeds, ip.numpy(), ix.numpy(), [15, 10, 5], False, ls)
+    for g, e in zip(got, exp):
+        for a, b in zip(g[1:], e[1:]):
+            assert np.array_equal(a.cpu().numpy(), b)
+    s_half = dgs.classes.P2PCacheSampler(ip, ix, torch.Tensor(), torch.arange(0, n, 2), 0)
+    assert ix.is_pinned()  # host rows remain: the registration is kept
+    del s_half
+    rng = np.random.default_rng(5)
+    data = torch.from_numpy(rng.standard_normal((n, 24)).astype(np.float32))
+    fs = dgs.classes.P2PCacheFeatureServer(data, torch.arange(n), 0)
+    assert not data.is_pinned()
+    q = rng.integers(0, n, 4096)
+    assert np.array_equal(fs._CAPI_get_feature(torch.from_numpy(q).cuda()).cpu().numpy(),
+                          O.index_select(data.numpy(), q))
