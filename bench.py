@@ -318,7 +318,7 @@ def timed_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist
     gc.disable()
     for _ in batches_of([next_seeds() for _ in range(args.warmup)]):
         pass
-    del _
+    _ = None  # (the last warm-up batch is not held into the timed region)
     # the timed batches' seeds (views of the shuffled train set, as SeedGenerator yields them)
     timed = [next_seeds() for _ in range(args.steps)]
     it = batches_of(timed)  # worker threads start here; no batch is submitted before t0
