@@ -1378,9 +1378,6 @@ __global__ __launch_bounds__(kTileRows) void k_bias_boot(BiasHubArgs a) {
 // does the hop's tile-offset scan (the rows / merge launch after it reads boff).  Row state is
 // kept in 32 bits (a row has < 2^31 edges, a lane's draw offset < 2^28, the hop's chunk count
 // and candidate room < 2^31): register pressure, not arithmetic, sets this kernel's occupancy.
-#ifndef DGS_STREAM_WINDOW
-#define DGS_STREAM_WINDOW 0
-#endif
 // DGS_STREAM_COUNTERS (diagnostic builds only): per half-wave candidate flushes, candidates
 // and row switches, summed per workgroup into the profiling stamps (DGS_PROF_HUB=1).
 #ifndef DGS_STREAM_COUNTERS
@@ -1514,32 +1511,6 @@ __device__ __forceinline__ void bias_stream_body(const BiasHubArgs &a, const int
     nb = 0;
   };
   load_row(h);
-#if DGS_STREAM_WINDOW
-  // Wide loads: the half-wave's lanes need steps qT - off_l + t (off_l < 4), all inside the
-  // window of steps [qT - 3, qT + T + 9): 384 consecutive probabilities, fetched as three 16-B
-  // loads per lane (3 load instructions instead of T), staged in this half-wave's LDS slice and
-  // read back per lane (conflict-free: consecutive lanes, consecutive words).  Used when the
-  // window lies inside the row; other chunks load per lane.
-  // (the window starts at the 16-B boundary at or below step qT - 3's first probability: `mis`
-  // floats earlier, at most 3, never before the array, whose base is 256-B aligned)
-  constexpr int kWin = 384;
-  __shared__ __attribute__((aligned(16))) float s_win[kTileRows / 32][kWin];
-  auto win_mis = [&](uint32_t q) {
-    return (int)(((uintptr_t)(pr + 32 * ((int64_t)q * kStreamT - 3)) & 15) >> 2);
-  };
-  auto win_ok = [&](uint32_t q) {
-    const int64_t w0 = (int64_t)q * kStreamT - 3;
-    return w0 >= 0 && 32 * w0 + kWin <= (int64_t)deg;
-  };
-  using f4v = float __attribute__((ext_vector_type(4)));
-  auto load_win = [&](uint32_t q, f4v *w) {
-    const global_ptr<f4v> pw = reinterpret_cast<global_ptr<f4v>>(
-        pr + 32 * ((int64_t)q * kStreamT - 3) - win_mis(q));
-#pragma unroll
-    for (int j = 0; j < 3; ++j) w[j] = pw[32 * j + l];
-  };
-  f4v wn[3];
-#endif
   // the next chunk's probabilities, loaded under this chunk's Philox (same row only)
   float pn[kStreamT];
   bool have_next = false;
@@ -1553,34 +1524,12 @@ __device__ __forceinline__ void bias_stream_body(const BiasHubArgs &a, const int
     const uint32_t q = ch - hstart;
     const int32_t i0 = chunk_i0(q);
     const bool whole = chunk_whole(i0);
-    float p[kStreamT];
-#if DGS_STREAM_WINDOW
-    if (win_ok(q)) {  // (half-wave uniform)
-      const int mis = win_mis(q);
-      if (!have_next) load_win(q, wn);
-      f4v *sw = reinterpret_cast<f4v *>(s_win[g]);
-#pragma unroll
-      for (int j = 0; j < 3; ++j) sw[32 * j + l] = wn[j];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-      for (int t = 0; t < kStreamT; ++t) p[t] = s_win[g][mis + (3 - (int)off + t) * 32 + l];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    } else {
-      load_probs(q, p);
-    }
-    have_next = ch + 1 < c1 && ch + 1 < hnext && win_ok(q + 1);
-    if (have_next) load_win(q + 1, wn);
-#else
     if (!have_next) load_probs(q, pn);
+    float p[kStreamT];
 #pragma unroll
     for (int t = 0; t < kStreamT; ++t) p[t] = pn[t];
     have_next = ch + 1 < c1 && ch + 1 < hnext;
     if (have_next) load_probs(q + 1, pn);
-#endif
     const uint32_t bc = (jb >> 2) + q * (kStreamT / 4);
     uint32_t xs[kStreamT];
 #pragma unroll
