@@ -31,4 +31,9 @@ for n, d in sorted(agg.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
         for k in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY"):
             if k in d:
                 line += f" {k[3:].lower()}/wave-cycles={d[k] / wc:.3f}"
+    known = {"SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES",
+             "SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY"}
+    for k in sorted(d):  # any other counter: its per-launch average
+        if k not in known:
+            line += f" {k}/launch={d[k] / c:.4g}"
     print(line)
