@@ -105,6 +105,9 @@ def parse(argv=None):
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--seed", type=int, default=20261015)
+    p.add_argument("--setup-timeout", type=float, default=900.0,
+                   help="N > 1: bound (s) of every setup / collective phase; a rank stalled "
+                        "longer exits non-zero naming the phase (DistGNN.dist.SetupWatchdog)")
     p.add_argument("--secondary", choices=["auto", "none", "papers_bias"], default="auto",
                    help="N = 1: also measure configs[3] (papers100M-like, biased) as a nested "
                         "record (auto: when the primary workload is the default one)")
@@ -413,17 +416,29 @@ def main():
     dev = torch.device("cuda", dev_index)
     dist = None
     comm = None
+    wd = None
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
+        from DistGNN.dist.watchdog import SetupWatchdog
+        # Bounded failure (round 6): a rank stalled in a collective -- rendezvous, the RCCL
+        # communicator, the services' IPC exchange, the self-check, the barriers around the
+        # timed region -- ends every rank non-zero within --setup-timeout s per phase, naming
+        # the phase, instead of holding the node until an outer limit.
+        wd = SetupWatchdog(args.setup_timeout, rank=rank, what="bench")
+        wd.step("init_process_group")
+        tmo = datetime.timedelta(seconds=args.setup_timeout)
         if share:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
     import dgs
     if world > 1:
         # the library's setup collectives (IPC handles, cache lists, barriers); none in the
         # timed loop.  Every mode sets it up, so the secondary replicated pass is collective too.
         comm = args.comm if args.comm != "auto" else ("gloo" if share else "rccl")
+        wd.step(f"library communicator ({comm})")
         if comm == "rccl":
             if share:
                 raise SystemExit("bench.py: RCCL refuses two ranks on one GPU; use --comm gloo")
@@ -433,7 +448,8 @@ def main():
             dgs.ops._CAPI_set_host_comm(dist.group.WORLD if share
                                         else dist.new_group(backend="gloo"))
 
-    out = run_workload(args, dgs, dist, world, rank, local_rank, mode, share, dev_index, dev, comm)
+    out = run_workload(args, dgs, dist, world, rank, local_rank, mode, share, dev_index, dev, comm,
+                       wd)
     sec = secondary_workload(args, world)
     if sec is not None:
         # configs[3] (papers100M-like graph, degree-weighted biased [15,10,5], d = 128) in the
@@ -454,8 +470,10 @@ def main():
         print(json.dumps(out), flush=True)
     torch.cuda.synchronize()
     if dist:
+        wd.step("final barrier")
         dist.barrier()
         dist.destroy_process_group()
+        wd.done()
 
 
 def secondary_workload(args, world):
@@ -475,13 +493,20 @@ def secondary_workload(args, world):
             "cpu_baseline_seconds": min(args.cpu_baseline_seconds, 8.0), "secondary": "none"}
 
 
-def run_workload(args, dgs, dist, world, rank, local_rank, mode, share, dev_index, dev, comm):
+def run_workload(args, dgs, dist, world, rank, local_rank, mode, share, dev_index, dev, comm,
+                 wd=None):
     """One workload's bench record: inputs, services, self-check (N > 1), the timed pass, side
-    passes and the CPU baseline; the services and inputs are freed before returning."""
+    passes and the CPU baseline; the services and inputs are freed before returning.  wd: the
+    N > 1 SetupWatchdog, told which phase this rank is in."""
     fan_out = [int(x) for x in args.fan_out.split(",")]
+
+    def phase(name):
+        if wd is not None:
+            wd.step(name)
 
     # ---------------- synthetic inputs (identical on every rank)
     t0 = time.time()
+    phase("inputs")
     if world > 1:
         port = os.environ.get("MASTER_PORT", "0")
         inp, host_copy = shared_inputs(args, dev, dist, local_rank,
@@ -513,6 +538,7 @@ def run_workload(args, dgs, dist, world, rank, local_rank, mode, share, dev_inde
     cached_mask = torch.zeros(N, dtype=torch.bool, device=dev)
     cached_mask[(hot if hot is not None else torch.arange(N)).to(dev)] = True
     t0 = time.time()
+    phase("services (cache build, IPC handle exchange)")
     sampler = dgs.classes.P2PCacheSampler(indptr, indices, probs, s_cache, dev_index)
     server = dgs.classes.P2PCacheFeatureServer(feats, f_cache, dev_index)
     labels_dev = labels.to(dev)
@@ -530,10 +556,12 @@ def run_workload(args, dgs, dist, world, rank, local_rank, mode, share, dev_inde
     # this layout's own sequential loop, and the xGMI pass samples with this layout's sampler)
     need_ref = not args.no_replicated_pass or args.check_batches > 0
     if world > 1 and mode != "replicated" and need_ref:
+        phase("replicated reference services")
         ref = (dgs.classes.P2PCacheSampler(indptr, indices, probs, everything, dev_index),
                dgs.classes.P2PCacheFeatureServer(feats, everything, dev_index))
     self_check = None
     if world > 1:
+        phase("multi-rank self-check")
         self_check = multi_rank_self_check(dgs, dist, sampler, server, ref, labels_dev, fan_out,
                                            args, next_seeds_factory(train_local, args), rank,
                                            world, dev, share)
@@ -542,6 +570,7 @@ def run_workload(args, dgs, dist, world, rank, local_rank, mode, share, dev_inde
     torch.manual_seed(1)
     next_seeds = next_seeds_factory(train_local, args)
 
+    phase("timed pass and side passes")
     elapsed, edges, rows, prof, step_gaps, mallocs = timed_pass(
         dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist, profile=True)
     row_bytes = args.dim * 4

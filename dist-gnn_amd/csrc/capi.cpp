@@ -229,6 +229,30 @@ int dgs_host_unregister(void *ptr) {
   });
 }
 
+int dgs_host_registrations(int64_t cap, uint64_t *bases, int64_t *bytes, int64_t *refs,
+                           int64_t *pins, int64_t *n_out) {
+  return guard([&] {
+    const std::vector<HostRegInfo> v = host_registrations();
+    *n_out = (int64_t)v.size();
+    for (int64_t i = 0; i < cap && i < (int64_t)v.size(); ++i) {
+      if (bases) bases[i] = v[i].base;
+      if (bytes) bytes[i] = v[i].bytes;
+      if (refs) refs[i] = v[i].refs;
+      if (pins) pins[i] = v[i].pins;
+    }
+  });
+}
+
+int dgs_host_memory_state(int64_t *n_registrations, int64_t *mirror_bytes,
+                          int64_t *n_mirrors) {
+  return guard([&] {
+    *n_registrations = (int64_t)host_registrations().size();
+    host_mirror_stats(mirror_bytes, n_mirrors);
+  });
+}
+
+int dgs_abi_version(void) { return DGS_ABI_VERSION; }
+
 // ------------------------------------------------------------------ async errors, streams
 int dgs_check_async_errors(void) {
   return guard([&] { check_async_errors(); });

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 
 #include "dgs_ops.h"
 
@@ -42,6 +43,11 @@ void Comm::init(int nranks, const void *unique_id, int rank) {
   DGS_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   DGS_HIP(hipMalloc(&dbuf_, sizeof(float)));
   DGS_HIP(hipMalloc(&dsizes_, sizeof(int64_t) * (kMaxDevices + 1)));
+  // Test switch: the own rank is a peer of the all-gathers like any other (ncclAllGather of the
+  // sizes, and a self ncclSend / ncclRecv pair in the payload group), so a one-GPU box runs the
+  // grouped send / recv path of NCCLTensorAllGather_ (nccl_context.cc:52-112).
+  const char *se = std::getenv("DGS_COMM_SELF_EXCHANGE");
+  self_exchange_ = se && se[0] == '1';
 }
 
 void Comm::init_host(int nranks, int rank, HostAllgatherFn ag, HostBarrierFn bar, void *ctx) {
@@ -68,7 +74,7 @@ void Comm::barrier() {
 
 std::vector<int64_t> Comm::allgather_sizes(int64_t mine) {
   std::vector<int64_t> out(world_, mine);
-  if (world_ == 1) return out;
+  if (world_ == 1 && !(comm_ && self_exchange_)) return out;
   if (host_ag_) {
     DGS_CHECK(host_ag_(&mine, sizeof(int64_t), out.data(), host_ctx_) == 0,
               "host allgather failed");
@@ -88,9 +94,10 @@ std::vector<int64_t> Comm::allgather_sizes(int64_t mine) {
 
 void Comm::allgather_bytes(const void *send, int64_t send_bytes, void *const *recv,
                            const int64_t *recv_bytes, hipStream_t st) {
-  if (recv[rank_] != send && send_bytes > 0)
+  const bool self = comm_ && self_exchange_ && !host_ag_;
+  if (!self && recv[rank_] != send && send_bytes > 0)
     DGS_HIP(hipMemcpyAsync(recv[rank_], send, send_bytes, hipMemcpyDeviceToDevice, st));
-  if (world_ == 1) return;
+  if (world_ == 1 && !self) return;
   if (host_ag_) {
     int64_t maxb = 1;
     for (int i = 0; i < world_; ++i) maxb = std::max(maxb, recv_bytes[i]);
@@ -105,13 +112,23 @@ void Comm::allgather_bytes(const void *send, int64_t send_bytes, void *const *re
   }
   if (!comm_) return;
   DGS_HIP(hipStreamSynchronize(st));
+  // self exchange into a buffer aliasing the payload: received into a temporary first
+  void *self_dst = nullptr;
+  if (self && send_bytes > 0)
+    self_dst = recv[rank_] == send ? nullptr : recv[rank_];
+  TmpBuf alias_tmp(self && send_bytes > 0 && !self_dst ? (size_t)send_bytes : 0, stream_);
+  if (self && send_bytes > 0 && !self_dst) self_dst = alias_tmp.p;
   DGS_NCCL(ncclGroupStart());
   for (int i = 0; i < world_; ++i) {
-    if (i == rank_) continue;
+    if (i == rank_ && !self) continue;
     DGS_NCCL(ncclSend(send, (size_t)send_bytes, ncclChar, i, comm_, stream_));
-    DGS_NCCL(ncclRecv(recv[i], (size_t)recv_bytes[i], ncclChar, i, comm_, stream_));
+    DGS_NCCL(ncclRecv(i == rank_ ? self_dst : recv[i], (size_t)recv_bytes[i], ncclChar, i, comm_,
+                      stream_));
   }
   DGS_NCCL(ncclGroupEnd());
+  if (self && self_dst == alias_tmp.p && send_bytes > 0)
+    DGS_HIP(hipMemcpyAsync(recv[rank_], alias_tmp.p, send_bytes, hipMemcpyDeviceToDevice,
+                           stream_));
   DGS_HIP(hipStreamSynchronize(stream_));
 }
 
@@ -139,9 +156,10 @@ bool is_device_pointer(const void *p) {
 }
 
 namespace {
-// Host ranges this library registered, with the number of live views into each: two services
-// over one host tensor share its registration, and the range is unregistered when the last of
-// them goes (unregistering it with the first would unmap the other's device view).
+// Host ranges this library registered (hipHostRegister), with the number of live references to
+// each.  Round 6: only dgs_host_register (_CAPI_tensor_pin_memory) registers caller memory; a
+// service over a pinned range holds a reference on it, so unpinning it first does not unmap the
+// service's view -- the range is unregistered when the last reference goes.
 struct HostReg {
   size_t bytes;
   int refs;
@@ -171,28 +189,52 @@ bool host_reg_overlaps(uintptr_t p, size_t n) {
   --it;                             // the last range starting before the end
   return it->first + it->second.bytes > p;
 }
+// whether a registered range shares a memory page with [p, p + n) (caller holds the lock).
+// hipHostRegister locks whole pages, so two registrations of neighbouring buffers that share a
+// page would lock, map and later unlock that page twice through different ranges: pins never
+// share a page.
+bool host_reg_shares_page(uintptr_t p, size_t n) {
+  const uintptr_t pg = 4096, lo = p & ~(pg - 1), hi = (p + n + pg - 1) & ~(pg - 1);
+  for (auto &kv : host_regs()) {
+    const uintptr_t rlo = kv.first & ~(pg - 1);
+    const uintptr_t rhi = (kv.first + kv.second.bytes + pg - 1) & ~(pg - 1);
+    if (rlo < hi && lo < rhi) return true;
+  }
+  return false;
+}
 // Pins taken through dgs_host_register, by the pointer the caller passed: an unregister must
 // name one of them (it cannot drop a reference a service holds).
 std::map<uintptr_t, int> &abi_pins() {
   static std::map<uintptr_t, int> m;
   return m;
 }
+// The first failed hipHostUnregister since the last check (raised by check_async_errors).  A
+// failed unregister leaves HIP's mapping of pages the caller is about to free, and a later
+// allocation at the same addresses would be taken for registered memory: it must not pass as a
+// stderr line (round 5 printed it, and pytest swallowed it for passing tests).
+std::string &host_reg_error() {
+  static std::string e;
+  return e;
+}
 void release_locked(const void *p) {
   auto it = host_reg_find(p);
   if (it == host_regs().end()) return;
   if (--it->second.refs == 0) {
-    // A failed unregister would leave HIP's mapping of pages the caller is about to free: a
-    // later allocation at the same addresses would then be taken for registered memory.  It
-    // cannot be raised from here (destructors), so it is reported.
     const hipError_t e = hipHostUnregister(reinterpret_cast<void *>(it->first));
     if (e != hipSuccess) {
       (void)hipGetLastError();
-      fprintf(stderr, "[dgs] warning: hipHostUnregister(%p, %zu bytes) failed: %s\n",
-              reinterpret_cast<void *>(it->first), it->second.bytes, hipGetErrorString(e));
+      if (host_reg_error().empty()) {
+        char buf[160];
+        snprintf(buf, sizeof(buf), "hipHostUnregister(%p, %zu bytes) failed: ",
+                 reinterpret_cast<void *>(it->first), it->second.bytes);
+        host_reg_error() = std::string(buf) + hipGetErrorString(e);
+      }
     }
     host_regs().erase(it);
   }
 }
+
+std::atomic<int64_t> g_mirror_bytes{0}, g_mirror_count{0};
 }  // namespace
 
 void release_host_view(const void *p) {
@@ -201,10 +243,42 @@ void release_host_view(const void *p) {
 }
 
 void host_pin(void *p, int64_t bytes) {
-  bool ref = false;
-  (void)device_view(p, bytes, &ref);
-  DGS_CHECK(ref, "host_register: the memory is already pinned outside this library");
+  DGS_CHECK(p && bytes > 0, "host_register: null pointer or empty range");
+  const size_t nb = (size_t)bytes;
   std::lock_guard<std::mutex> g(host_reg_mu());
+  auto it = host_reg_find(p);
+  if (it != host_regs().end() && (uintptr_t)p + nb <= it->first + it->second.bytes) {
+    ++it->second.refs;  // inside a range pinned here already: share it
+  } else {
+    // A range that only partly lies in a registration cannot be mapped: HIP refuses a second
+    // registration of the same pages.
+    DGS_CHECK(!host_reg_overlaps((uintptr_t)p, nb),
+              "host range overlaps a registration made for a different range of the same "
+              "buffer; register (pin) the whole buffer first");
+    DGS_CHECK(!host_reg_shares_page((uintptr_t)p, nb),
+              "host range shares a memory page with another pinned range; pin one buffer that "
+              "holds both, or use page-aligned buffers (torch pin_memory())");
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) == hipSuccess) {
+      DGS_CHECK(a.type != hipMemoryTypeHost,
+                "host_register: the memory is already pinned outside this library");
+      DGS_CHECK(a.type != hipMemoryTypeDevice && a.type != hipMemoryTypeManaged &&
+                    a.type != hipMemoryTypeUnified,
+                "host_register: device memory");
+    } else {
+      (void)hipGetLastError();
+    }
+    // pin_memory.cc:7-12 registers the tensor's own range (cudaHostRegisterDefault); mapped
+    // here, so kernels read it through the device pointer
+    DGS_HIP(hipHostRegister(p, nb, hipHostRegisterMapped));
+    void *d = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&d, p, 0);
+    if (e != hipSuccess) {
+      (void)hipHostUnregister(p);
+      DGS_HIP(e);
+    }
+    host_regs()[(uintptr_t)p] = HostReg{nb, 1};
+  }
   ++abi_pins()[(uintptr_t)p];
 }
 
@@ -218,53 +292,131 @@ void host_unpin(void *p) {
   release_locked(p);
 }
 
-void *device_view(const void *p, int64_t bytes, bool *registered_here) {
-  if (registered_here) *registered_here = false;
+void *pinned_view(const void *p, int64_t bytes, bool *pin_ref) {
+  if (pin_ref) *pin_ref = false;
   if (!p) return nullptr;
   const size_t nb = (size_t)(bytes > 0 ? bytes : 1);
-  std::lock_guard<std::mutex> g(host_reg_mu());
   {
+    std::lock_guard<std::mutex> g(host_reg_mu());
     auto it = host_reg_find(p);
     if (it != host_regs().end() && (uintptr_t)p + nb <= it->first + it->second.bytes) {
-      // a range registered here already: share it
+      // inside a dgs_host_register pin: read in place, holding a reference on it
       void *d = nullptr;
       DGS_HIP(hipHostGetDevicePointer(&d, reinterpret_cast<void *>(it->first), 0));
       ++it->second.refs;
-      if (registered_here) *registered_here = true;
+      if (pin_ref) *pin_ref = true;
       return static_cast<char *>(d) + ((uintptr_t)p - it->first);
     }
-    // A range that only partly lies in one of this library's registrations cannot be mapped:
-    // a second registration over the same pages is refused by HIP, and the pointer query below
-    // would return a view of the registered part only, with no reference held on it.
     DGS_CHECK(!host_reg_overlaps((uintptr_t)p, nb),
-              "host range overlaps a registration made for a different range of the same "
-              "buffer; register (pin) the whole buffer first");
+              "host range overlaps a pinned range it does not lie in; pin the whole buffer "
+              "first");
   }
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) == hipSuccess) {
     if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
         a.type == hipMemoryTypeUnified)
       return const_cast<void *>(p);
-    if (a.type == hipMemoryTypeHost) {
+    if (a.type == hipMemoryTypeHost) {  // pinned by its owner (torch pin_memory, hipHostMalloc)
       void *d = nullptr;
       if (hipHostGetDevicePointer(&d, const_cast<void *>(p), 0) == hipSuccess && d) return d;
       (void)hipGetLastError();
-      return a.devicePointer ? a.devicePointer : const_cast<void *>(p);
+      if (a.devicePointer) return a.devicePointer;
     }
   } else {
     (void)hipGetLastError();
   }
-  // pageable host memory: register it (mapped) for zero-copy device reads
-  DGS_HIP(hipHostRegister(const_cast<void *>(p), nb, hipHostRegisterMapped));
-  void *d = nullptr;
-  const hipError_t e = hipHostGetDevicePointer(&d, const_cast<void *>(p), 0);
-  if (e != hipSuccess) {
-    (void)hipHostUnregister(const_cast<void *>(p));
-    DGS_HIP(e);
+  return nullptr;  // pageable
+}
+
+std::vector<HostRegInfo> host_registrations() {
+  std::lock_guard<std::mutex> g(host_reg_mu());
+  std::vector<HostRegInfo> v;
+  for (auto &kv : host_regs()) {
+    auto pin = abi_pins().find(kv.first);
+    v.push_back(HostRegInfo{kv.first, (int64_t)kv.second.bytes, kv.second.refs,
+                            pin == abi_pins().end() ? 0 : pin->second});
   }
-  host_regs()[(uintptr_t)p] = HostReg{nb, 1};
-  if (registered_here) *registered_here = true;
-  return d;
+  return v;
+}
+
+void host_mirror_stats(int64_t *bytes, int64_t *count) {
+  *bytes = g_mirror_bytes.load();
+  *count = g_mirror_count.load();
+}
+
+// ------------------------------------------------------------------ host staging
+void host_copy(void *dst, const void *src, size_t bytes) {
+  constexpr size_t kPart = size_t(32) << 20;
+  if (bytes < 2 * kPart) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  // a few threads: one core copies pageable memory at ~10 GB/s, well below the memory system
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t nt = std::min<size_t>({(size_t)16, (size_t)hw, bytes / kPart});
+  const size_t per = (bytes / nt + 4095) & ~size_t(4095);
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; ++t) {
+    const size_t lo = t * per;
+    if (lo >= bytes) break;
+    const size_t n = std::min(per, bytes - lo);
+    th.emplace_back([=] { std::memcpy((char *)dst + lo, (const char *)src + lo, n); });
+  }
+  std::memcpy(dst, src, std::min(per, bytes));
+  for (auto &t : th) t.join();
+}
+
+namespace {
+// Two library-owned pinned staging buffers for uploads of pageable host memory (allocated on
+// first use, kept for the process).
+constexpr size_t kStageBytes = size_t(128) << 20;
+struct Staging {
+  std::mutex mu;
+  void *buf[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+};
+Staging &staging() {
+  static Staging s;
+  return s;
+}
+}  // namespace
+
+void upload_pageable(void *dst, const void *src, size_t bytes, hipStream_t st) {
+  if (bytes == 0) return;
+  Staging &S = staging();
+  std::lock_guard<std::mutex> g(S.mu);
+  for (int i = 0; i < 2; ++i) {
+    if (!S.buf[i]) DGS_HIP(hipHostMalloc(&S.buf[i], kStageBytes, hipHostMallocDefault));
+    if (!S.done[i]) DGS_HIP(hipEventCreateWithFlags(&S.done[i], hipEventDisableTiming));
+  }
+  // chunk c: wait until the DMA that last read staging buffer c & 1 is done, fill it on the
+  // host, enqueue its copy (the host fills the other buffer while the DMA runs)
+  bool used[2] = {false, false};
+  for (size_t off = 0, c = 0; off < bytes; off += kStageBytes, ++c) {
+    const int b = (int)(c & 1);
+    const size_t n = std::min(kStageBytes, bytes - off);
+    if (used[b]) DGS_HIP(hipEventSynchronize(S.done[b]));
+    host_copy(S.buf[b], (const char *)src + off, n);
+    DGS_HIP(hipMemcpyAsync((char *)dst + off, S.buf[b], n, hipMemcpyHostToDevice, st));
+    DGS_HIP(hipEventRecord(S.done[b], st));
+    used[b] = true;
+  }
+  DGS_HIP(hipStreamSynchronize(st));
+}
+
+void *mirror_alloc(size_t bytes) {
+  void *h = nullptr;
+  DGS_HIP(hipHostMalloc(&h, bytes ? bytes : 1, hipHostMallocMapped));
+  g_mirror_bytes += (int64_t)bytes;
+  g_mirror_count += 1;
+  return h;
+}
+
+void mirror_free(void *h, size_t bytes) {
+  if (!h) return;
+  (void)hipHostFree(h);
+  g_mirror_bytes -= (int64_t)bytes;
+  g_mirror_count -= 1;
 }
 
 // ------------------------------------------------------------------ async errors
@@ -297,6 +449,15 @@ int64_t *async_err_dev() { return async_err().dev; }
 uint64_t async_err_next_tag() { return async_err().tag.fetch_add(1) + 1; }
 
 void check_async_errors() {
+  {
+    std::lock_guard<std::mutex> g(host_reg_mu());
+    if (!host_reg_error().empty()) {
+      const std::string e = host_reg_error();
+      host_reg_error().clear();
+      throw Error("host memory: " + e + " (a registration of this library outlived its "
+                  "release; its pages stay mapped)");
+    }
+  }
   AsyncErrWords &w = async_err();
   const int64_t kind = __atomic_load_n(&w.host[0], __ATOMIC_ACQUIRE);
   if (kind == 0) return;

@@ -76,20 +76,40 @@ class Comm {
   hipStream_t stream_ = nullptr;
   float *dbuf_ = nullptr;
   int64_t *dsizes_ = nullptr;
+  bool self_exchange_ = false;  // DGS_COMM_SELF_EXCHANGE=1 at init (tests)
 };
 
-// Device-accessible pointer for `p`: device memory is returned as is; pinned / registered
-// host memory is translated; pageable host memory is registered (mapped) first and
-// *registered_here is set so the owner can unregister it.
-// *registered_here = true: the view holds a reference on a registration made by this library
-// (shared by every view into the range); release it with release_host_view(p).
-// A range that partly overlaps one of this library's registrations is refused (Error).
-void *device_view(const void *p, int64_t bytes, bool *registered_here);
+// Host memory.  Round 6: the library never registers pageable caller memory for a service
+// (DESIGN.md section 3).  What a service reads from the host is either pinned by its owner
+// (read in place) or a library-owned copy (a device temporary for the cache build, or a pinned
+// mirror for rows that stay on the host); only dgs_host_register registers caller memory.
+//
+// Device-accessible pointer for `p` when it needs no copy: device memory, host memory pinned by
+// its owner, or a range inside a dgs_host_register pin (then *pin_ref = true: the caller holds
+// a reference, released with release_host_view(p)).  nullptr for pageable memory.  A range
+// that partly overlaps a pin is refused (Error).
+void *pinned_view(const void *p, int64_t bytes, bool *pin_ref);
 void release_host_view(const void *p);
 // dgs_host_register / dgs_host_unregister: a reference on the registration plus a pin keyed by
 // `p`; unpinning a pointer that holds no pin is an error.
 void host_pin(void *p, int64_t bytes);
 void host_unpin(void *p);
+struct HostRegInfo {
+  uintptr_t base;
+  int64_t bytes;
+  int refs;  // pins + service views
+  int pins;  // dgs_host_register pins keyed by base
+};
+std::vector<HostRegInfo> host_registrations();
+// Library-owned copies of host arrays: a multi-threaded memcpy; an upload of pageable memory to
+// device memory through two library-owned pinned staging buffers (HIP's own pageable-copy path
+// is not used for the caller's arrays); pinned, mapped mirrors (hipHostMalloc) counted for
+// diagnostics (dgs_host_memory_state).
+void host_copy(void *dst, const void *src, size_t bytes);
+void upload_pageable(void *dst, const void *src, size_t bytes, hipStream_t st);
+void *mirror_alloc(size_t bytes);
+void mirror_free(void *h, size_t bytes);
+void host_mirror_stats(int64_t *bytes, int64_t *count);
 bool is_device_pointer(const void *p);
 
 // Out-of-range ids met by the gather kernels (feature server, index_select, the loader's fused
@@ -102,6 +122,7 @@ constexpr int64_t kAsyncErrFeature = 1, kAsyncErrLabel = 2, kAsyncErrSelect = 3;
 constexpr int kAsyncErrWords = 4;
 int64_t *async_err_dev();  // device-visible address of the words (allocated on first use)
 uint64_t async_err_next_tag();  // per-process call counter (the tag a launch reports)
-void check_async_errors();     // throws (and clears) when a kernel stored an error
+// throws (and clears) when a kernel stored an error, or when a pin's hipHostUnregister failed
+void check_async_errors();
 
 }  // namespace dgs

@@ -56,6 +56,9 @@ int64_t count_out_of_range(const int64_t *list, int64_t n, int64_t num_rows, hip
 int64_t count_in_range(const int64_t *tab, int64_t n, const void *lo, int64_t bytes,
                        hipStream_t st);
 int64_t count_loc(const NodeEntry *tab, int64_t n, int loc, hipStream_t st);
+// rows of [0, num_rows) that none of the lists (device arrays, counts[l] ids each) names
+int64_t count_uncovered(const int64_t *const *lists, const int64_t *counts, int nlists,
+                        int64_t num_rows, hipStream_t st);
 // ftab[nids[i]] = base + i * row_bytes (ids outside [0, num_rows) are skipped)
 void ftab_assign(int64_t *ftab, int64_t num_rows, const int64_t *nids, int64_t n,
                  const void *base, int64_t row_bytes, hipStream_t st);

@@ -413,23 +413,53 @@ __global__ void k_count_loc(const NodeEntry *tab, int64_t n, int loc, unsigned l
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
 }
 
+// ids of a list, marked in a byte per row (ids outside [0, num_rows) are skipped)
+__global__ void k_mark_ids(const int64_t *list, int64_t n, int64_t num_rows, uint8_t *mark) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t v = list[i];
+  if ((uint64_t)v < (uint64_t)num_rows) mark[v] = 1;
+}
+
+__global__ void k_count_unmarked(const uint8_t *mark, int64_t n, unsigned long long *cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool un = i < n && mark[i] == 0;
+  const unsigned long long c = __popcll(__ballot(un));
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
+}
+
+// A count made on the device and read back (setup-time checks).  Every error is raised: the
+// callers take 0 as the permissive answer (a cache list accepted, a host array released), so a
+// failed launch, copy or synchronisation must not read as 0.  The counter is a TmpBuf (freed
+// after a stream synchronisation also when this throws).
 template <typename K, typename... A>
 int64_t count_on_device(K kernel, int64_t n, hipStream_t st, A... args) {
   if (n <= 0) return 0;
-  unsigned long long *bad = nullptr, h = 0;
-  DGS_HIP(hipMalloc(&bad, sizeof(*bad)));
-  DGS_HIP(hipMemsetAsync(bad, 0, sizeof(*bad), st));
-  hipLaunchKernelGGL(kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, args..., bad);
-  const hipError_t le = hipGetLastError();
-  if (le == hipSuccess) {
-    (void)hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, st);
-    (void)hipStreamSynchronize(st);
-  }
-  (void)hipFree(bad);
-  DGS_HIP(le);
+  TmpBuf bad(sizeof(unsigned long long), st);
+  unsigned long long h = 0;
+  DGS_HIP(hipMemsetAsync(bad.p, 0, sizeof(h), st));
+  hipLaunchKernelGGL(kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, args...,
+                     bad.as<unsigned long long>());
+  DGS_LAUNCH_CHECK();
+  DGS_HIP(hipMemcpyAsync(&h, bad.p, sizeof(h), hipMemcpyDeviceToHost, st));
+  DGS_HIP(hipStreamSynchronize(st));
   return (int64_t)h;
 }
 }  // namespace
+
+int64_t count_uncovered(const int64_t *const *lists, const int64_t *counts, int nlists,
+                        int64_t num_rows, hipStream_t st) {
+  if (num_rows <= 0) return 0;
+  TmpBuf mark((size_t)num_rows, st);
+  DGS_HIP(hipMemsetAsync(mark.p, 0, (size_t)num_rows, st));
+  for (int l = 0; l < nlists; ++l) {
+    if (counts[l] <= 0) continue;
+    hipLaunchKernelGGL(k_mark_ids, dim3((unsigned)ceil_div(counts[l], 256)), dim3(256), 0, st,
+                       lists[l], counts[l], num_rows, mark.as<uint8_t>());
+    DGS_LAUNCH_CHECK();
+  }
+  return count_on_device(k_count_unmarked, num_rows, st, mark.as<const uint8_t>(), num_rows);
+}
 
 int64_t count_stride_mismatch(const int64_t *list, int64_t n, int64_t start, int64_t stride,
                               hipStream_t st) {

@@ -93,6 +93,43 @@ static int64_t *device_copy_ids(const int64_t *ids, int64_t n, hipStream_t st) {
   return d;
 }
 
+// ============================================================== host sources
+void HostSource::attach(const void *p, int64_t bytes, bool keep, hipStream_t st) {
+  release();
+  if (!p || bytes <= 0) return;
+  bool ref = false;
+  if (void *v = pinned_view(p, bytes, &ref)) {
+    dev = v;
+    if (ref) pin_ = p;
+    return;
+  }
+  bytes_ = (size_t)bytes;
+  if (!keep) {
+    // the build reads it from HBM; half the free memory stays for the caches it builds
+    size_t free_b = 0, total_b = 0;
+    DGS_HIP(hipMemGetInfo(&free_b, &total_b));
+    if (bytes_ <= free_b / 2) {
+      DGS_HIP(hipMalloc(&dtemp_, bytes_));
+      dev = dtemp_;
+      upload_pageable(dtemp_, p, bytes_, st);
+      return;
+    }
+  }
+  mirror_ = mirror_alloc(bytes_);
+  host_copy(mirror_, p, bytes_);
+  DGS_HIP(hipHostGetDevicePointer(&dev, mirror_, 0));
+}
+
+void HostSource::release() {
+  if (pin_) release_host_view(pin_);
+  if (dtemp_) (void)hipFree(dtemp_);
+  if (mirror_) mirror_free(mirror_, bytes_);
+  pin_ = nullptr;
+  dtemp_ = mirror_ = nullptr;
+  dev = nullptr;
+  bytes_ = 0;
+}
+
 // ============================================================== Sampler
 Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *probs,
                  int64_t num_nodes, int64_t num_edges, const int64_t *cache_nids,
@@ -119,18 +156,32 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
   if (const char *e = std::getenv("DGS_SAMPLER_MAX_CTX"))
     max_ctx_ = (size_t)std::max(1, std::atoi(e));
   hipStream_t st = nullptr;
-  h_indptr_.attach(indptr, (num_nodes + 1) * 8);
-  h_indices_.attach(indices, num_edges * 8);
-  if (bias_) h_probs_.attach(probs, num_edges * 4);
-  const int64_t *d_indptr = (const int64_t *)h_indptr_.dev;
 
-  // this rank's cached sub-CSR (sampler.cc:89-110).  A cached id outside [0, num_nodes) is
-  // refused here (the reference reads indptr out of bounds, utils.cu:12-42).
+  // this rank's cache list, shared with every rank first: it decides what the build needs.  A
+  // cached id outside [0, num_nodes) is refused (the reference reads indptr out of bounds,
+  // utils.cu:12-42).
   int64_t *nids = device_copy_ids(cache_nids, n_cache, st);
   if (count_out_of_range(nids, n_cache, num_nodes, st) != 0) {
     (void)hipFree(nids);
     DGS_CHECK(false, "cache_nids: an id is outside [0, num_nodes)");
   }
+  nids_srv_ = P2PServer::adopt(nids, n_cache, 8);
+  // Rows no GPU caches are read from the host while the sampler lives (a pinned mirror of the
+  // neighbour ids / probabilities); with none, the host graph only feeds the cache build (a
+  // device temporary).  indptr is only read by the build.
+  std::vector<const int64_t *> lists(world_);
+  std::vector<int64_t> counts(world_);
+  for (int d = 0; d < world_; ++d) {
+    lists[d] = (const int64_t *)nids_srv_->ptr(d);
+    counts[d] = nids_srv_->items(d);
+  }
+  const bool host_rows = count_uncovered(lists.data(), counts.data(), world_, num_nodes, st) > 0;
+  h_indptr_.attach(indptr, (num_nodes + 1) * 8, /*keep=*/false, st);
+  h_indices_.attach(indices, num_edges * 8, host_rows, st);
+  if (bias_) h_probs_.attach(probs, num_edges * 4, host_rows, st);
+  const int64_t *d_indptr = (const int64_t *)h_indptr_.dev;
+
+  // this rank's cached sub-CSR (sampler.cc:89-110)
   int64_t *sub_indptr = nullptr;
   DGS_HIP(hipMalloc(&sub_indptr, sizeof(int64_t) * (size_t)(n_cache + 1)));
   extract_indptr(nids, n_cache, d_indptr, sub_indptr, st);
@@ -149,7 +200,6 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
   indptr_srv_ = P2PServer::adopt(sub_indptr, n_cache + 1, 8);
   indices_srv_ = P2PServer::adopt(sub_indices, n_sub, 8);
   if (bias_) probs_srv_ = P2PServer::adopt(sub_probs, n_sub, 4);
-  nids_srv_ = P2PServer::adopt(nids, n_cache, 8);
 
   // graph shard context: node table (replaces CreateNidsP2PCacheHashMapCUDA, hashmap.cu)
   ntab_.ensure(sizeof(NodeEntry) * (size_t)(num_nodes > 0 ? num_nodes : 1));
@@ -160,6 +210,14 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
                 (const int64_t *)indptr_srv_->ptr(d), nids_srv_->items(d), d,
                 (const int64_t *)indices_srv_->ptr(d), st);
   DGS_HIP(hipStreamSynchronize(st));
+  // the table's host pointers name exactly the uncovered rows
+  DGS_CHECK((count_loc(ntab, num_nodes, kLocHost, st) > 0) == host_rows,
+            "sampler: node table and cache coverage disagree");
+  h_indptr_.release();
+  if (!host_rows) {
+    h_indices_.release();
+    h_probs_.release();
+  }
 
   src_.ntab = ntab;
   src_.indptr = nullptr;
@@ -171,14 +229,6 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
   for (int d = 0; d < world_; ++d) {
     src_.indices_base.p[d] = indices_srv_->ptr(d);
     src_.probs.p[d] = bias_ ? probs_srv_->ptr(d) : nullptr;
-  }
-  // Every row cached on some GPU: the host graph was only read to build the caches, so its
-  // registration (pinned, mapped pages: the whole host CSR) is released now instead of being
-  // held for the sampler's life.
-  if (count_loc(ntab, num_nodes, kLocHost, st) == 0) {
-    h_indptr_.detach();
-    h_indices_.detach();
-    h_probs_.detach();
   }
   src_.indices_base.p[kLocHost] = h_indices_.dev;
   src_.probs.p[kLocHost] = bias_ ? h_probs_.dev : nullptr;
@@ -619,7 +669,6 @@ FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_byt
   num_rows_ = num_rows;
   row_bytes_ = row_bytes;
   hipStream_t st = nullptr;
-  h_data_.attach(data, num_rows * row_bytes);
   int64_t *nids = device_copy_ids(cache_nids, n_cache, st);
   // a cached id outside [0, num_rows) is refused (the reference's hashmap would take it and
   // its gather read out of bounds, feature_server.cc:10-61)
@@ -627,12 +676,9 @@ FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_byt
     (void)hipFree(nids);
     DGS_CHECK(false, "cache_nids: an id is outside [0, num_rows)");
   }
-  void *block = nullptr;
-  DGS_HIP(hipMalloc(&block, (size_t)(n_cache * row_bytes > 0 ? n_cache * row_bytes : 1)));
-  gather_plain(h_data_.dev, num_rows, row_bytes, nids, 8, n_cache, block, st);
-  DGS_HIP(hipStreamSynchronize(st));
-  feat_srv_ = P2PServer::adopt(block, n_cache, row_bytes);
-
+  // every rank's cache list (NCCLTensorAllGather_), first: rows no GPU caches are read from the
+  // host while the server lives (a pinned mirror); with none, the host matrix only fills the
+  // caches (a device temporary)
   std::vector<int64_t> nbytes(world_, n_cache * 8);
   DGS_CHECK(world_ <= kMaxDevices, "at most 8 GPUs");
   std::vector<void *> lists(world_, nullptr);
@@ -641,11 +687,25 @@ FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_byt
   } else {
     lists[0] = nids;
   }
+  std::vector<const int64_t *> lp(world_);
+  std::vector<int64_t> counts(world_);
+  for (int d = 0; d < world_; ++d) {
+    lp[d] = (const int64_t *)lists[d];
+    counts[d] = nbytes[d] / 8;
+  }
+  const bool host_rows = count_uncovered(lp.data(), counts.data(), world_, num_rows, st) > 0;
+  h_data_.attach(data, num_rows * row_bytes, host_rows, st);
+  void *block = nullptr;
+  DGS_HIP(hipMalloc(&block, (size_t)(n_cache * row_bytes > 0 ? n_cache * row_bytes : 1)));
+  gather_plain(h_data_.dev, num_rows, row_bytes, nids, 8, n_cache, block, st);
+  DGS_HIP(hipStreamSynchronize(st));
+  feat_srv_ = P2PServer::adopt(block, n_cache, row_bytes);
+
   ftab_.ensure(sizeof(int64_t) * (size_t)(num_rows > 0 ? num_rows : 1));
   int64_t *ftab = ftab_.as<int64_t>();
   // absolute row addresses: host rows first, then every GPU's cache (local last = priority)
   ftab_init(ftab, num_rows, h_data_.dev, row_bytes, st);
-  align_or_ = (uintptr_t)h_data_.dev;
+  align_or_ = host_rows ? (uintptr_t)h_data_.dev : 0;
   for (int d : rotation(rank_, world_)) {
     ftab_assign(ftab, num_rows, (const int64_t *)lists[d], nbytes[d] / 8, feat_srv_->ptr(d),
                 row_bytes, st);
@@ -656,12 +716,12 @@ FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_byt
   if (world_ > 1)
     for (void *p : lists) DGS_HIP(hipFree(p));
   DGS_HIP(hipFree(nids));
-  // Every row cached on some GPU: the host matrix was only read to fill the caches; its
-  // registration is released (the alignment test no longer counts the host base).
-  if (count_in_range(ftab, num_rows, h_data_.dev, num_rows * row_bytes, st) == 0) {
-    h_data_.detach();
-    align_or_ = 0;
-    for (int d : rotation(rank_, world_)) align_or_ |= (uintptr_t)feat_srv_->ptr(d);
+  if (!host_rows) {
+    // every row is cached on some GPU: no entry of the table names the host source
+    DGS_CHECK(!h_data_.dev || num_rows * row_bytes == 0 ||
+                  count_in_range(ftab, num_rows, h_data_.dev, num_rows * row_bytes, st) == 0,
+              "feature server: address table and cache coverage disagree");
+    h_data_.release();
   }
 }
 

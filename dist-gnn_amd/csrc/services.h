@@ -44,22 +44,31 @@ class P2PServer {
   int rank_ = 0, world_ = 1;
 };
 
-// Registers host memory for the object's lifetime when the caller did not pin it.
-struct HostView {
-  const void *host = nullptr;
-  void *dev = nullptr;
-  bool registered_here = false;
-  void attach(const void *p, int64_t bytes) {
-    host = p;
-    dev = device_view(p, bytes, &registered_here);
-  }
-  // drops this view's registration reference (no device read may follow)
-  void detach() {
-    if (registered_here) release_host_view(host);
-    registered_here = false;
-    dev = nullptr;
-  }
-  ~HostView() { detach(); }
+// A caller's host array as a service's kernels read it (sampler CSR and probabilities, feature
+// matrix).  Pageable caller memory is never registered (round 6):
+//  - keep == false (every row is cached on some GPU: the array only feeds the cache build): a
+//    device temporary filled through the library's pinned staging (a pinned mirror when the
+//    device lacks room), dropped by release() once the caches are built;
+//  - keep == true (rows stay on the host and are read zero-copy while the service lives): a
+//    library-owned pinned, mapped mirror (hipHostMalloc) holding a copy.
+// Device memory, and host memory pinned by its owner or by dgs_host_register (then a
+// reference is held on that pin), are read in place.
+struct HostSource {
+  void *dev = nullptr;  // device-accessible address of the array (nullptr: empty)
+  HostSource() = default;
+  HostSource(const HostSource &) = delete;
+  HostSource &operator=(const HostSource &) = delete;
+  void attach(const void *p, int64_t bytes, bool keep, hipStream_t st);
+  // no device read of `dev` may follow (the caller synchronises first)
+  void release();
+  bool host_resident() const { return mirror_ != nullptr || pin_ != nullptr; }
+  ~HostSource() { release(); }
+
+ private:
+  const void *pin_ = nullptr;  // a dgs_host_register range holding our reference
+  void *dtemp_ = nullptr;      // device temporary (hipMalloc)
+  void *mirror_ = nullptr;     // pinned mirror (hipHostMalloc)
+  size_t bytes_ = 0;
 };
 
 class Sampler {
@@ -102,7 +111,7 @@ class Sampler {
   int64_t num_nodes_ = 0, num_edges_ = 0;
   int rank_ = 0, world_ = 1;
   bool bias_ = false;
-  HostView h_indptr_, h_indices_, h_probs_;
+  HostSource h_indptr_, h_indices_, h_probs_;
   P2PServer *indptr_srv_ = nullptr, *indices_srv_ = nullptr, *probs_srv_ = nullptr;
   P2PServer *nids_srv_ = nullptr;
   DevBuf ntab_;
@@ -177,7 +186,7 @@ class FeatureServer {
  private:
   int64_t num_rows_ = 0, row_bytes_ = 0;
   int rank_ = 0, world_ = 1;
-  HostView h_data_;
+  HostSource h_data_;
   P2PServer *feat_srv_ = nullptr;
   void detect_strided(const std::vector<void *> &lists, const std::vector<int64_t> &nbytes,
                       hipStream_t st);

@@ -45,6 +45,10 @@ _SIGS = {
     "dgs_set_random_seed": (c_int, [c_u64]),
     "dgs_host_register": (c_int, [c_vp, c_i64]),
     "dgs_host_unregister": (c_int, [c_vp]),
+    "dgs_host_registrations": (c_int, [c_i64, ctypes.POINTER(c_u64), p_i64, p_i64, p_i64,
+                                       p_i64]),
+    "dgs_host_memory_state": (c_int, [p_i64, p_i64, p_i64]),
+    "dgs_abi_version": (c_int, []),
     "dgs_index_select": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_i64, c_vp, c_vp]),
     "dgs_index_select_device": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_i64, c_vp, c_vp]),
     "dgs_check_async_errors": (c_int, []),
@@ -99,6 +103,11 @@ for _name, (_res, _args) in _SIGS.items():
     _f.argtypes = _args
 
 EXPORTED = sorted(_SIGS)
+
+ABI_VERSION = 6  # include/dgs_amd.h DGS_ABI_VERSION, the argument lists in _SIGS
+if lib.dgs_abi_version() != ABI_VERSION:
+    raise ImportError(f"dgs: {LIB_PATH} has ABI revision {lib.dgs_abi_version()}, this binding "
+                      f"expects {ABI_VERSION}: rebuild the library")
 
 
 def check(rc):

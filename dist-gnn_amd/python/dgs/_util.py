@@ -56,33 +56,6 @@ def check_cpu(t, name):
         raise RuntimeError(f"{name} must be a CPU tensor")
 
 
-def pin_storages(tensors):
-    """Registers the whole host storage of every pageable CPU tensor in `tensors` and returns
-    the registered base pointers (release them with unpin_storages).  A service over a view of
-    a buffer (data[:k]) then maps the buffer's single registration, which any later service over
-    another view of the same buffer shares, instead of a partial range the library would have
-    to refuse for that second service."""
-    from ._lib import check, lib
-    pins = []
-    try:
-        for t in tensors:
-            if t is None or t.is_cuda or t.numel() == 0 or t.is_pinned():
-                continue
-            st = t.untyped_storage()
-            check(lib.dgs_host_register(c_vp(st.data_ptr()), st.nbytes()))
-            pins.append(st.data_ptr())
-    except Exception:
-        unpin_storages(pins)
-        raise
-    return pins
-
-
-def unpin_storages(pins):
-    from ._lib import lib
-    for p in pins:
-        lib.dgs_host_unregister(c_vp(p))
-
-
 def row_bytes(t):
     stride = 1
     for s in t.shape[1:]:

@@ -8,8 +8,7 @@ import ctypes
 import torch
 
 from ._lib import c_i64, c_vp, check, i64_array, lib, stream_ptr, vp_array
-from ._util import (as_i64, check_cpu, check_cuda, device_view, pin_storages, ptr, row_bytes,
-                    unpin_storages)
+from ._util import as_i64, check_cpu, check_cuda, device_view, ptr, row_bytes
 
 
 def _host_i64(t, name):
@@ -88,12 +87,10 @@ class P2PCacheSampler:
         self._keep.append(cn)
         self.num_nodes = ip.numel() - 1
         h = c_vp()
-        pins = pin_storages((ip, ix, pr))
-        try:
-            check(lib.dgs_sampler_create(ptr(ip), ptr(ix), ptr(pr), self.num_nodes, ix.numel(),
-                                         ptr(cn), cn.numel(), int(device_id), ctypes.byref(h)))
-        finally:  # the sampler holds its own references on the registrations
-            unpin_storages(pins)
+        # pageable host arrays are copied by the library (never registered in place); pinned
+        # ones (pin_memory(), _CAPI_tensor_pin_memory) are read in place
+        check(lib.dgs_sampler_create(ptr(ip), ptr(ix), ptr(pr), self.num_nodes, ix.numel(),
+                                     ptr(cn), cn.numel(), int(device_id), ctypes.byref(h)))
         self._h = h
         self._plans = {}
         self.device = torch.device("cuda", torch.cuda.current_device())
@@ -292,12 +289,8 @@ class P2PCacheFeatureServer:
         cn = cache_nids.to(torch.int64).contiguous()
         self._keep.append(cn)
         h = c_vp()
-        pins = pin_storages((d,))
-        try:
-            check(lib.dgs_feature_server_create(ptr(d), d.shape[0], self._row_bytes, ptr(cn),
-                                                cn.numel(), int(device_id), ctypes.byref(h)))
-        finally:  # the server holds its own reference on the registration
-            unpin_storages(pins)
+        check(lib.dgs_feature_server_create(ptr(d), d.shape[0], self._row_bytes, ptr(cn),
+                                            cn.numel(), int(device_id), ctypes.byref(h)))
         self._h = h
         self.device = torch.device("cuda", torch.cuda.current_device())
 

@@ -267,6 +267,30 @@ def _check_async_errors():
     check(lib.dgs_check_async_errors())
 
 
+def _host_registrations():
+    """ADDITIVE (diagnostics, tests): the library's live host registrations as a list of
+    dicts {base, bytes, refs, pins}.  Only _CAPI_tensor_pin_memory registers caller memory;
+    services copy pageable arrays instead."""
+    n = c_i64()
+    check(lib.dgs_host_registrations(0, None, None, None, None, ctypes.byref(n)))
+    k = n.value
+    if k == 0:
+        return []
+    bases, nb = (ctypes.c_uint64 * k)(), (c_i64 * k)()
+    refs, pins = (c_i64 * k)(), (c_i64 * k)()
+    check(lib.dgs_host_registrations(k, bases, nb, refs, pins, ctypes.byref(n)))
+    return [{"base": int(bases[i]), "bytes": int(nb[i]), "refs": int(refs[i]),
+             "pins": int(pins[i])} for i in range(min(k, n.value))]
+
+
+def _host_memory_state():
+    """ADDITIVE (diagnostics, tests): {registrations, mirror_bytes, mirrors} -- live
+    registrations and the library's pinned host mirrors (services with host-resident rows)."""
+    r, b, m = c_i64(), c_i64(), c_i64()
+    check(lib.dgs_host_memory_state(ctypes.byref(r), ctypes.byref(b), ctypes.byref(m)))
+    return {"registrations": r.value, "mirror_bytes": b.value, "mirrors": m.value}
+
+
 def _stream_create(priority=0):
     """ADDITIVE: a new non-blocking HIP stream (int handle) owned by the caller; hand it to
     torch with torch.cuda.ExternalStream.  Unlike torch's pooled streams it is never given to

@@ -16,6 +16,8 @@
  *    computed on the device (marked SYNC) synchronise `stream` once.
  *  - Device arrays: pointers usable by the current HIP device (device memory, or host
  *    memory registered with dgs_host_register / allocated pinned).
+ *  - Host arrays handed to a service constructor (graph, features) may be pageable: the
+ *    library copies what it needs and never registers them (dgs_host_register below).
  *  - Ids and CSR offsets are int64 unless an `*_bytes` argument says otherwise.
  */
 #ifndef DGS_AMD_H_
@@ -70,12 +72,30 @@ int dgs_set_random_seed(uint64_t seed);
 /* ------------------------------------------------------------------------------------
  * Host memory registration (src/common/pin_memory.cc:7-19; pybind.cc:57-58)
  * ---------------------------------------------------------------------------------- */
-/* Registrations are reference counted and shared with the host views of the services (a
- * sampler or feature server over pageable host memory registers it the same way): unregister
- * drops this call's reference, and the range is unmapped when the last reference goes.
- * Memory pinned outside this library (hipHostMalloc, torch pin_memory) is refused. */
+/* hipHostRegister (mapped) of [ptr, ptr + bytes) in place, as pin_memory.cc:7-12.  These pins are
+ * the only caller memory the library registers: a sampler or feature server over pageable host
+ * memory copies what it reads (a device temporary for the cache build, or a library-owned
+ * pinned mirror for rows that stay on the host), and one over a pinned
+ * range reads it in place, holding a reference on the pin.  Unregister drops this call's
+ * reference; the range is unmapped when the last reference goes.  A failed hipHostUnregister is
+ * reported by the next dgs_check_async_errors (and gather entry point).  Memory pinned outside
+ * this library (hipHostMalloc, torch pin_memory) is refused, as is a range that partly
+ * overlaps a pin. */
 int dgs_host_register(void *ptr, int64_t bytes);
 int dgs_host_unregister(void *ptr);
+/* ADDITIVE (diagnostics, tests): the library's live registrations -- base, bytes, references
+ * (pins + service views) and pins keyed by the base -- up to `cap` entries (any array may be
+ * NULL); *n_out = their number. */
+int dgs_host_registrations(int64_t cap, uint64_t *bases, int64_t *bytes, int64_t *refs,
+                           int64_t *pins, int64_t *n_out);
+/* ADDITIVE (diagnostics, tests): number of live registrations, and the bytes / number of the
+ * library's pinned host mirrors (services with rows left on the host). */
+int dgs_host_memory_state(int64_t *n_registrations, int64_t *mirror_bytes, int64_t *n_mirrors);
+/* ADDITIVE: the ABI revision of this header (DGS_ABI_VERSION).  Round 5 inserted num_rows /
+ * label_rows arguments into dgs_index_select, dgs_index_select_device and dgs_loader_gather;
+ * a binding checks this at load time instead of passing shifted arguments. */
+#define DGS_ABI_VERSION 6
+int dgs_abi_version(void);
 
 /* ------------------------------------------------------------------------------------
  * Stateless ops (pybind.cc:53-76)
@@ -169,8 +189,8 @@ int dgs_p2p_server_destroy(dgs_p2p_server *s); /* collective when world_size > 1
  * P2PCacheSampler (src/sampling/sampler.{h,cc}; pybind.cc:21-31)
  * ---------------------------------------------------------------------------------- */
 typedef struct dgs_sampler dgs_sampler;
-/* indptr[num_nodes+1], indices[num_edges], probs[num_edges] or NULL: host arrays (registered
- * by the library when not already pinned) -- sampler.cc:64-136.  cache_nids: this rank's
+/* indptr[num_nodes+1], indices[num_edges], probs[num_edges] or NULL: host arrays (pageable
+ * ones are copied: see dgs_host_register) -- sampler.cc:64-136.  cache_nids: this rank's
  * cached node ids (device or host; an id outside [0, num_nodes) is refused).  Collective when
  * world_size > 1.  Destruction waits for the sampler's calls and the device's queued work. */
 int dgs_sampler_create(const int64_t *indptr, const int64_t *indices, const float *probs,
@@ -253,7 +273,7 @@ int dgs_sampler_destroy(dgs_sampler *s); /* collective when world_size > 1 */
  * P2PCacheFeatureServer (src/feature/feature_server.cc, feature_sever.h; pybind.cc:33-39)
  * ---------------------------------------------------------------------------------- */
 typedef struct dgs_feature_server dgs_feature_server;
-/* data: host array [num_rows, row_bytes] (registered by the library when not pinned);
+/* data: host array [num_rows, row_bytes] (copied when pageable: see dgs_host_register);
  * cache_nids: rows cached in this GPU's HBM (device or host; an id outside [0, num_rows) is
  * refused).  feature_server.cc:10-61.  Destruction waits for the device's queued work. */
 int dgs_feature_server_create(const void *data, int64_t num_rows, int64_t row_bytes,

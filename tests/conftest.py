@@ -44,3 +44,10 @@ def _gpu_test_drained(request):
     torch.cuda.synchronize()
     import dgs
     dgs.ops._check_async_errors()
+    # No library registration outlives its users: the only registrations are the pins
+    # _CAPI_tensor_pin_memory still holds (services copy pageable arrays instead, DESIGN.md
+    # section 3), so once those are dropped the table is empty.  The table goes into the report.
+    regs = dgs.ops._host_registrations()
+    pinned = {base for _, base in dgs.ops._registered.values()}
+    stray = [r for r in regs if r["base"] not in pinned]
+    assert not stray, f"host registrations outlived their users: {regs}"

@@ -563,15 +563,22 @@ def test_standalone_ops_on_two_streams(dgs):
             assert torch.equal(a, b)
 
 
-def test_shared_host_registration_outlives_first_owner(dgs):
-    """Two services over one pageable host tensor share the library's registration of it: the
-    first one's destruction must not unmap the second's device view (refcounted registry)."""
+def test_services_over_one_pageable_tensor_are_independent(dgs):
+    """Two services over one pageable host tensor: each holds its own library-owned copy of what
+    it reads (round 6: pageable caller memory is never registered), so destroying the first
+    leaves the second exact, and no registration exists at any point."""
     import gc
     rng = np.random.default_rng(4)
     data = torch.from_numpy(rng.standard_normal((2000, 64)).astype(np.float32))
-    assert not data.is_pinned()
+    base = dgs.ops._host_memory_state()
     a = dgs.classes.P2PCacheFeatureServer(data, torch.tensor([5]), 0)
     b = dgs.classes.P2PCacheFeatureServer(data, torch.tensor([9]), 0)
+    st = dgs.ops._host_memory_state()
+    assert st["registrations"] == base["registrations"] == 0
+    # partly cached: each keeps a pinned mirror of the matrix for its host rows
+    assert st["mirrors"] == base["mirrors"] + 2
+    assert st["mirror_bytes"] == base["mirror_bytes"] + 2 * data.numel() * 4
+    assert not data.is_pinned()
     q = rng.integers(0, 2000, 4096)
     exp = O.index_select(data.numpy(), q)
     assert np.array_equal(a._CAPI_get_feature(_cuda(q)).cpu().numpy(), exp)
@@ -581,30 +588,37 @@ def test_shared_host_registration_outlives_first_owner(dgs):
     assert np.array_equal(b._CAPI_get_feature(_cuda(q)).cpu().numpy(), exp)
     del b
     gc.collect()
-    # all views gone: the range is unregistered, a new service registers it again
+    assert dgs.ops._host_memory_state() == base
     c = dgs.classes.P2PCacheFeatureServer(data, torch.tensor([1]), 0)
     assert np.array_equal(c._CAPI_get_feature(_cuda(q)).cpu().numpy(), exp)
 
 
 def test_unpin_keeps_a_live_service_mapped(dgs):
-    """_CAPI_tensor_pin_memory / unpin share the services' refcounted registrations: unpinning a
-    tensor a feature server still reads leaves the server's view mapped."""
+    """A service over a _CAPI_tensor_pin_memory tensor reads it in place, holding a reference on
+    the pin: unpinning the tensor while the server reads it leaves the server's view mapped, and
+    the registration goes with the server."""
     import gc
     rng = np.random.default_rng(6)
     data = torch.from_numpy(rng.standard_normal((1500, 32)).astype(np.float32))
     dgs.ops._CAPI_tensor_pin_memory(data)
     fs = dgs.classes.P2PCacheFeatureServer(data, torch.tensor([3]), 0)
+    regs = dgs.ops._host_registrations()
+    assert [(r["base"], r["refs"], r["pins"]) for r in regs] == [(data.data_ptr(), 2, 1)]
+    assert dgs.ops._host_memory_state()["mirrors"] == 0  # in place, no copy
     dgs.ops._CAPI_tensor_unpin_memory(data)
     gc.collect()
+    assert [(r["refs"], r["pins"]) for r in dgs.ops._host_registrations()] == [(1, 0)]
     q = rng.integers(0, 1500, 2048)
     assert np.array_equal(fs._CAPI_get_feature(_cuda(q)).cpu().numpy(),
                           O.index_select(data.numpy(), q))
+    del fs
+    gc.collect()
+    assert dgs.ops._host_registrations() == []
 
 
-def test_overlapping_views_share_one_registration(dgs):
-    """Services over different views of one pageable buffer (data[:k], then data) map the
-    buffer's single registration: destroying the first leaves the second's rows mapped and
-    byte-exact (the binding registers whole storages, pin_memory.cc:7-19)."""
+def test_services_over_views_of_one_buffer(dgs):
+    """Services over different views of one pageable buffer (data[:k], data, data[k:]) copy their
+    own ranges: destroying the first leaves the others byte-exact, with no registration."""
     import gc
     rng = np.random.default_rng(8)
     data = torch.from_numpy(rng.standard_normal((3000, 48)).astype(np.float32))
@@ -612,6 +626,7 @@ def test_overlapping_views_share_one_registration(dgs):
     a = dgs.classes.P2PCacheFeatureServer(data[:k], torch.tensor([2]), 0)
     b = dgs.classes.P2PCacheFeatureServer(data, torch.tensor([7]), 0)
     c = dgs.classes.P2PCacheFeatureServer(data[k:], torch.tensor([0]), 0)
+    assert dgs.ops._host_registrations() == []
     qa, qb = rng.integers(0, k, 2048), rng.integers(0, 3000, 4096)
     assert np.array_equal(a._CAPI_get_feature(_cuda(qa)).cpu().numpy(),
                           O.index_select(data[:k].numpy(), qa))
@@ -626,13 +641,13 @@ def test_overlapping_views_share_one_registration(dgs):
 
 
 def test_c_abi_registration_rules(dgs):
-    """At the C ABI: a range that only partly lies in a registration the library made is
-    refused (no unreferenced, partly unmapped view), an unregister must name a pointer that
-    dgs_host_register pinned, and a contained range shares the registration."""
+    """At the C ABI: a range that only partly lies in a pin is refused (no unreferenced, partly
+    unmapped view), as is one that shares a memory page with a pin; an unregister must name a
+    pointer that dgs_host_register pinned, and a contained range shares the registration."""
     import ctypes
     from dgs._lib import lib
     buf = torch.zeros(1 << 16, dtype=torch.uint8)
-    base = buf.data_ptr()
+    base = (buf.data_ptr() + 4095) // 4096 * 4096 + 4096  # page aligned, inside buf
     assert lib.dgs_host_register(ctypes.c_void_p(base), 4096) == 0
     # starts inside the registration, ends past it
     assert lib.dgs_host_register(ctypes.c_void_p(base + 1024), 8192) != 0
@@ -640,15 +655,28 @@ def test_c_abi_registration_rules(dgs):
     # a service over such a range is refused the same way
     with pytest.raises(RuntimeError, match="overlaps"):
         _raw_feature_server(base + 1024, 256, 32)
+    # disjoint bytes, shared page: refused (a pin of [q, q + 100) and one of [q + 200, ...))
+    q = base + 3 * 4096
+    assert lib.dgs_host_register(ctypes.c_void_p(q), 100) == 0
+    assert lib.dgs_host_register(ctypes.c_void_p(q + 200), 100) != 0
+    assert b"shares a memory page" in lib.dgs_last_error()
+    assert lib.dgs_host_unregister(ctypes.c_void_p(q)) == 0
+    # the page after the first pin is free
+    assert lib.dgs_host_register(ctypes.c_void_p(base + 4096), 4096) == 0
+    assert lib.dgs_host_unregister(ctypes.c_void_p(base + 4096)) == 0
     # contained: shares, and needs its own unregister
     assert lib.dgs_host_register(ctypes.c_void_p(base + 512), 1024) == 0
+    regs = dgs.ops._host_registrations()
+    assert [(r["base"], r["bytes"], r["refs"], r["pins"]) for r in regs] == [(base, 4096, 2, 1)]
     assert lib.dgs_host_unregister(ctypes.c_void_p(base + 7)) != 0  # never pinned
     assert lib.dgs_host_unregister(ctypes.c_void_p(base + 512)) == 0
     assert lib.dgs_host_unregister(ctypes.c_void_p(base + 512)) != 0  # already released
     assert lib.dgs_host_unregister(ctypes.c_void_p(base)) == 0
+    assert dgs.ops._host_registrations() == []
     # everything released: the larger range registers cleanly now
     assert lib.dgs_host_register(ctypes.c_void_p(base + 1024), 8192) == 0
     assert lib.dgs_host_unregister(ctypes.c_void_p(base + 1024)) == 0
+    dgs.ops._check_async_errors()  # no failed unregister was recorded
 
 
 def _raw_feature_server(ptr, rows, row_bytes):

@@ -188,29 +188,43 @@ def test_pending_call_of_a_destroyed_sampler_raises(dgs):
     assert lib.dgs_feature_server_destroy(None) == 0
 
 
-def test_fully_cached_services_release_the_host_registration(dgs):
-    """A sampler / feature server whose rows are all cached on the GPU reads its host arrays
-    only while it builds the caches: the library's registration of them (pinned, mapped pages)
-    is released at once, and the services stay exact.  A partly cached one keeps it."""
+def test_services_never_register_pageable_memory(dgs):
+    """Round 6: a sampler / feature server over pageable host arrays never
+    registers them.  Fully cached, the arrays only feed the cache build (a device temporary,
+    gone when the constructor returns); partly cached, the service reads its host rows from a
+    library-owned pinned mirror that goes with it.  Both stay exact against the oracle, the
+    caller's tensors stay pageable, and the library holds no registration throughout."""
+    import gc
     from oracle import oracle as O
     ip, ix = _small_graph(2000, seed=3)
     n = ip.numel() - 1
-    s_all = dgs.classes.P2PCacheSampler(ip, ix, torch.Tensor(), torch.arange(n), 0)
-    assert not ix.is_pinned() and not ip.is_pinned()
+    base = dgs.ops._host_memory_state()
+    assert base["registrations"] == 0
     seeds = np.random.default_rng(4).permutation(n)[:300]
     ls = [101, 202, 303]
-    got = s_all._sample_seeded(torch.from_numpy(seeds).cuda(), [15, 10, 5], False, ls)
     exp = O.node_classification_sample(seeds, ip.numpy(), ix.numpy(), [15, 10, 5], False, ls)
-    for g, e in zip(got, exp):
-        for a, b in zip(g[1:], e[1:]):
-            assert np.array_equal(a.cpu().numpy(), b)
-    s_half = dgs.classes.P2PCacheSampler(ip, ix, torch.Tensor(), torch.arange(0, n, 2), 0)
-    assert ix.is_pinned()  # host rows remain: the registration is kept
-    del s_half
+    for cache, mirrors in ((torch.arange(n), 0), (torch.arange(0, n, 2), 1)):
+        s = dgs.classes.P2PCacheSampler(ip, ix, torch.Tensor(), cache, 0)
+        st = dgs.ops._host_memory_state()
+        assert st["registrations"] == 0 and st["mirrors"] == base["mirrors"] + mirrors
+        assert not ix.is_pinned() and not ip.is_pinned()
+        got = s._sample_seeded(torch.from_numpy(seeds).cuda(), [15, 10, 5], False, ls)
+        for g, e in zip(got, exp):
+            for a, b in zip(g[1:], e[1:]):
+                assert np.array_equal(a.cpu().numpy(), b)
+        del s, got
+        gc.collect()
+        assert dgs.ops._host_memory_state() == base
     rng = np.random.default_rng(5)
     data = torch.from_numpy(rng.standard_normal((n, 24)).astype(np.float32))
-    fs = dgs.classes.P2PCacheFeatureServer(data, torch.arange(n), 0)
-    assert not data.is_pinned()
     q = rng.integers(0, n, 4096)
-    assert np.array_equal(fs._CAPI_get_feature(torch.from_numpy(q).cuda()).cpu().numpy(),
-                          O.index_select(data.numpy(), q))
+    for cache, mirrors in ((torch.arange(n), 0), (torch.arange(1, n, 3), 1)):
+        fs = dgs.classes.P2PCacheFeatureServer(data, cache, 0)
+        st = dgs.ops._host_memory_state()
+        assert st["registrations"] == 0 and st["mirrors"] == base["mirrors"] + mirrors
+        assert not data.is_pinned()
+        assert np.array_equal(fs._CAPI_get_feature(torch.from_numpy(q).cuda()).cpu().numpy(),
+                              O.index_select(data.numpy(), q))
+        del fs
+        gc.collect()
+        assert dgs.ops._host_memory_state() == base

@@ -18,8 +18,7 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.fixture(scope="module")
-def res():
+def _run_worker(*extra):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -28,10 +27,32 @@ def res():
         out = os.path.join(td, "r.json")
         env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        rc = subprocess.run([sys.executable, os.path.join(HERE, "rccl_worker.py"), out],
+        rc = subprocess.run([sys.executable, os.path.join(HERE, "rccl_worker.py"), out, *extra],
                             env=env, timeout=180).returncode
         assert rc == 0
         return json.load(open(out))
+
+
+@pytest.fixture(scope="module")
+def res():
+    return _run_worker()
+
+
+@pytest.fixture(scope="module")
+def res_self():
+    return _run_worker("self")
+
+
+def test_rccl_grouped_send_recv_self_exchange(res_self):
+    """The grouped ncclSend / ncclRecv all-gather (nccl_context.cc:52-112) executed on the GPU:
+    with the own rank as a peer, the world-1 communicator moves every payload through RCCL."""
+    assert res_self["world"] == 1
+    assert res_self["sizes"] == [12345]
+    assert res_self["bytes_equal"] and res_self["bytes_nonzero"] > 3 * (1 << 20) * 0.99
+    assert res_self["allgather"] == [[x + 0.5 for x in range(7)]]
+    assert res_self["feature_kat"] == [[float(x) for x in range(b, b + 10)]
+                                       for b in (0, 30, 50, 70)]
+    assert res_self["barrier_rc"] == 0
 
 
 def test_rccl_communicator_world1(res):
