@@ -258,6 +258,10 @@ int dgs_check_async_errors(void) {
   return guard([&] { check_async_errors(); });
 }
 
+int dgs_last_gather_tag(uint64_t *tag) {
+  return guard([&] { *tag = async_err_last_tag(); });
+}
+
 int dgs_stream_create(int priority, void **out) {
   return guard([&] {
     hipStream_t st = nullptr;
@@ -460,13 +464,15 @@ int dgs_compute_frontier_heat_fixed(const int64_t *seeds, int64_t n_seeds,
                                     float *frontier_heat, void *stream) {
   return guard([&] {
     hipStream_t st = S(stream);
-    // the int64 accumulator is this call's own allocation, freed once the stream has run the
-    // kernels that use it: nothing another op or stream runs can overwrite it
-    TmpBuf acc(sizeof(uint64_t) * (size_t)(num_nodes > 0 ? num_nodes : 1), st);
+    // the int64 accumulator lives in the stream's op scratch (stream-asynchronous: calls on one
+    // stream are ordered by it, calls on other streams use their own scratch)
+    HopScratch *ws = nullptr;
+    const OpScratchLease lk = op_scratch(st, &ws);
+    ws->op_tmp.ensure(sizeof(uint64_t) * (size_t)(num_nodes > 0 ? num_nodes : 1));
     heat(dev_ptr(seeds, "seeds"), n_seeds, dev_ptr(indptr, "indptr"),
          dev_ptr(indices, "indices"), dev_ptr(probs, "probs"),
          dev_ptr(seeds_heat, "seeds_heat"), num_picks, indptr_diff, frontier_heat, num_nodes,
-         acc.as<unsigned long long>(), st);
+         ws->op_tmp.as<unsigned long long>(), st);
   });
 }
 

@@ -446,7 +446,14 @@ AsyncErrWords &async_err() {
 
 int64_t *async_err_dev() { return async_err().dev; }
 
-uint64_t async_err_next_tag() { return async_err().tag.fetch_add(1) + 1; }
+namespace {
+thread_local uint64_t t_last_tag = 0;
+}
+uint64_t async_err_next_tag() {
+  t_last_tag = async_err().tag.fetch_add(1) + 1;
+  return t_last_tag;
+}
+uint64_t async_err_last_tag() { return t_last_tag; }
 
 void check_async_errors() {
   {

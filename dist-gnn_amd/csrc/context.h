@@ -122,6 +122,7 @@ constexpr int64_t kAsyncErrFeature = 1, kAsyncErrLabel = 2, kAsyncErrSelect = 3;
 constexpr int kAsyncErrWords = 4;
 int64_t *async_err_dev();  // device-visible address of the words (allocated on first use)
 uint64_t async_err_next_tag();  // per-process call counter (the tag a launch reports)
+uint64_t async_err_last_tag();  // the tag of this thread's last gather launch (0: none)
 // throws (and clears) when a kernel stored an error, or when a pin's hipHostUnregister failed
 void check_async_errors();
 

@@ -10,6 +10,7 @@ sampling context per stream over the shared graph.
 """
 import collections
 import os
+import re
 import threading
 import time
 
@@ -110,6 +111,10 @@ class PrefetchLoader:
         self._pulled = collections.deque()
         self._events = [torch.cuda.Event() for _ in range(depth + 2)]
         self._ev_n = 0
+        # (gather call tag, batch index) of the batches handed out: an out-of-range report
+        # names its launch's tag, which maps back to the batch
+        self._tags = collections.deque(maxlen=4096)
+        self._handed = 0
 
     def _caller_stream(self):
         if _raw_stream is not None:
@@ -190,6 +195,11 @@ class PrefetchLoader:
             self._submit(cur)
         if not self._inflight:
             self.close()  # returns the streams
+            # The gathers' range reports of this loader's batches, the last one's included: its
+            # kernels have run once the caller's stream has (the epoch's end; one wait)
+            if self._handed:
+                torch.cuda.current_stream(self.device).synchronize()
+                self._check_reports()
             raise StopIteration
         pending, s64, w = self._inflight.popleft()
         st = self._st[w]
@@ -222,9 +232,18 @@ class PrefetchLoader:
         if self.labels is not None:
             y = torch.empty((s64.numel(),) + tuple(self.labels.shape[1:]),
                             dtype=self.labels.dtype, device=self.device)
-        # (the sampler's launches recorded the event this wait uses: no record here)
-        dgs.ops._loader_gather(self.sampler if blocks else None, self.server, st, cur, front, x,
-                               self.labels, self._label_row_bytes, s64, y)
+        # (the sampler's launches recorded the event this wait uses: no record here).  The
+        # entry point first raises a range report of an earlier batch's gathers: the loader
+        # then closes (in-flight calls ended, streams returned) and names that batch.
+        try:
+            dgs.ops._loader_gather(self.sampler if blocks else None, self.server, st, cur, front,
+                                   x, self.labels, self._label_row_bytes, s64, y)
+        except RuntimeError as e:
+            self.close()
+            raise RuntimeError(self._attribute(str(e))) from None
+        if x is not None or y is not None:
+            self._tags.append((dgs.ops._last_gather_tag(), self._handed))
+        self._handed += 1
         dt = self.sampler._id_dtype
         if dt != torch.int64:  # int32 graphs: cast on the caller's stream, now ordered after B
             cast, cur_seeds = [], blocks[0][0]
@@ -236,6 +255,28 @@ class PrefetchLoader:
         if _TRACE:
             self.trace.append(("gathers", time.perf_counter()))
         return blocks, x, y
+
+    def _attribute(self, msg):
+        m = re.search(r"gather call #(\d+)", msg)
+        if m:
+            tag = int(m.group(1))
+            for t, i in self._tags:
+                if t == tag:
+                    return f"{msg} [PrefetchLoader batch {i}]"
+        return msg
+
+    def _check_reports(self):
+        try:
+            dgs.ops._check_async_errors()
+        except RuntimeError as e:
+            raise RuntimeError(self._attribute(str(e))) from None
+
+    def check(self):
+        """Waits for the caller's current stream, then raises (naming the batch) if a gather of
+        this loader -- or of anything else in the process since the last check -- met an id
+        outside its source's rows.  The loader also does this when it is exhausted."""
+        torch.cuda.current_stream(self.device).synchronize()
+        self._check_reports()
 
     def close(self):
         """Ends the calls still in flight (a stream takes a new call only after its last one

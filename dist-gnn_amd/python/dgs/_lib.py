@@ -52,6 +52,7 @@ _SIGS = {
     "dgs_index_select": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_i64, c_vp, c_vp]),
     "dgs_index_select_device": (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_i64, c_vp, c_vp]),
     "dgs_check_async_errors": (c_int, []),
+    "dgs_last_gather_tag": (c_int, [ctypes.POINTER(c_u64)]),
     "dgs_stream_create": (c_int, [c_int, p_vp]),
     "dgs_stream_destroy": (c_int, [c_vp]),
     "dgs_stream_wait": (c_int, [c_vp, c_vp]),

@@ -267,6 +267,13 @@ def _check_async_errors():
     check(lib.dgs_check_async_errors())
 
 
+def _last_gather_tag():
+    """ADDITIVE: the call tag ("gather call #") of this thread's last gather launch."""
+    t = ctypes.c_uint64()
+    check(lib.dgs_last_gather_tag(ctypes.byref(t)))
+    return t.value
+
+
 def _host_registrations():
     """ADDITIVE (diagnostics, tests): the library's live host registrations as a list of
     dicts {base, bytes, refs, pins}.  Only _CAPI_tensor_pin_memory registers caller memory;

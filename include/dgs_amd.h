@@ -116,6 +116,10 @@ int dgs_index_select_device(const void *data, int64_t num_rows, int64_t row_byte
  * source's rows since the last check; clears the report.  No synchronisation: the report of a
  * kernel still queued appears once it has run. */
 int dgs_check_async_errors(void);
+/* ADDITIVE: the call tag of the calling thread's last gather launch -- the "gather call #"
+ * an out-of-range report names -- so a caller can tell which of its batches reported (0: no
+ * gather launched on this thread yet). */
+int dgs_last_gather_tag(uint64_t *tag);
 /* ADDITIVE: a non-blocking HIP stream owned by the caller (hipStreamCreateWithPriority;
  * priority 0 = default, lower = higher priority), for a loader's batch streams: unlike a
  * framework's pooled streams it is never handed to anyone else. */

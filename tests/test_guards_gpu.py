@@ -94,14 +94,40 @@ def test_loader_label_rows_out_of_range_are_reported(dgs):
     _drain_errors(dgs)
     seeds = [torch.tensor([1, 2, 3], device="cuda"), torch.tensor([4, 250, 6], device="cuda")]
     got = []
-    with pytest.raises(RuntimeError, match="label gather .* outside \\[0, 100\\)"):
+    # the bad seed is in the last batch: the loader itself raises when it is exhausted, naming
+    # the batch (no explicit check by the caller)
+    with pytest.raises(RuntimeError, match="label gather .* outside \\[0, 100\\).*batch 1\\]"):
         for blocks, x, y in PrefetchLoader(sampler, seeds, [5], server=srv, labels=labels,
                                            depth=2):
             got.append(y.cpu())
-        torch.cuda.synchronize()
-        dgs.ops._check_async_errors()
     assert got[0].tolist() == [3, 6, 9]
     assert got[1].tolist() == [12, 0, 18]
+    dgs.ops._check_async_errors()  # reported once
+
+
+def test_loader_names_the_batch_of_a_bad_id_and_closes(dgs):
+    """A bad id in batch 0 of four is raised by the loader at a later batch's gather entry point
+    -- naming batch 0 -- and the loader has closed (its streams are back in the pool)."""
+    from DistGNN.dataloading import PrefetchLoader
+    from DistGNN.dataloading import prefetch as P
+    ip, ix = _small_graph()
+    n = ip.numel() - 1
+    sampler = dgs.classes.P2PCacheSampler(ip, ix, torch.Tensor(), torch.arange(n), 0)
+    srv = dgs.classes.P2PCacheFeatureServer(torch.randn(n, 8), torch.arange(n), 0)
+    labels = torch.arange(100, dtype=torch.int64, device="cuda")
+    _drain_errors(dgs)
+    seeds = [torch.tensor([1, 500, 3], device="cuda")] + \
+        [torch.tensor([4, 5, 6], device="cuda")] * 3
+    free0 = len(P._FREE_STREAMS.get(torch.device("cuda", 0), []))
+    loader = PrefetchLoader(sampler, seeds, [5], server=srv, labels=labels, depth=2)
+    handed = 0
+    with pytest.raises(RuntimeError, match="outside \\[0, 100\\).*batch 0\\]"):
+        for _ in loader:
+            handed += 1
+            torch.cuda.synchronize()  # batch 0's report is in before the next gather entry
+    assert handed == 1
+    assert loader._streams == [] and not loader._inflight
+    assert len(P._FREE_STREAMS.get(torch.device("cuda", 0), [])) >= free0 + 2
 
 
 def test_cache_lists_outside_the_graph_are_refused(dgs):
@@ -198,15 +224,15 @@ def test_services_never_register_pageable_memory(dgs):
     from oracle import oracle as O
     ip, ix = _small_graph(2000, seed=3)
     n = ip.numel() - 1
-    base = dgs.ops._host_memory_state()
-    assert base["registrations"] == 0
+    base = dgs.ops._host_memory_state()  # (pins of earlier tests may live on)
     seeds = np.random.default_rng(4).permutation(n)[:300]
     ls = [101, 202, 303]
     exp = O.node_classification_sample(seeds, ip.numpy(), ix.numpy(), [15, 10, 5], False, ls)
     for cache, mirrors in ((torch.arange(n), 0), (torch.arange(0, n, 2), 1)):
         s = dgs.classes.P2PCacheSampler(ip, ix, torch.Tensor(), cache, 0)
         st = dgs.ops._host_memory_state()
-        assert st["registrations"] == 0 and st["mirrors"] == base["mirrors"] + mirrors
+        assert st["registrations"] == base["registrations"]
+        assert st["mirrors"] == base["mirrors"] + mirrors
         assert not ix.is_pinned() and not ip.is_pinned()
         got = s._sample_seeded(torch.from_numpy(seeds).cuda(), [15, 10, 5], False, ls)
         for g, e in zip(got, exp):
@@ -221,7 +247,8 @@ def test_services_never_register_pageable_memory(dgs):
     for cache, mirrors in ((torch.arange(n), 0), (torch.arange(1, n, 3), 1)):
         fs = dgs.classes.P2PCacheFeatureServer(data, cache, 0)
         st = dgs.ops._host_memory_state()
-        assert st["registrations"] == 0 and st["mirrors"] == base["mirrors"] + mirrors
+        assert st["registrations"] == base["registrations"]
+        assert st["mirrors"] == base["mirrors"] + mirrors
         assert not data.is_pinned()
         assert np.array_equal(fs._CAPI_get_feature(torch.from_numpy(q).cuda()).cpu().numpy(),
                               O.index_select(data.numpy(), q))
