@@ -189,19 +189,6 @@ bool host_reg_overlaps(uintptr_t p, size_t n) {
   --it;                             // the last range starting before the end
   return it->first + it->second.bytes > p;
 }
-// whether a registered range shares a memory page with [p, p + n) (caller holds the lock).
-// hipHostRegister locks whole pages, so two registrations of neighbouring buffers that share a
-// page would lock, map and later unlock that page twice through different ranges: pins never
-// share a page.
-bool host_reg_shares_page(uintptr_t p, size_t n) {
-  const uintptr_t pg = 4096, lo = p & ~(pg - 1), hi = (p + n + pg - 1) & ~(pg - 1);
-  for (auto &kv : host_regs()) {
-    const uintptr_t rlo = kv.first & ~(pg - 1);
-    const uintptr_t rhi = (kv.first + kv.second.bytes + pg - 1) & ~(pg - 1);
-    if (rlo < hi && lo < rhi) return true;
-  }
-  return false;
-}
 // Pins taken through dgs_host_register, by the pointer the caller passed: an unregister must
 // name one of them (it cannot drop a reference a service holds).
 std::map<uintptr_t, int> &abi_pins() {
@@ -255,9 +242,6 @@ void host_pin(void *p, int64_t bytes) {
     DGS_CHECK(!host_reg_overlaps((uintptr_t)p, nb),
               "host range overlaps a registration made for a different range of the same "
               "buffer; register (pin) the whole buffer first");
-    DGS_CHECK(!host_reg_shares_page((uintptr_t)p, nb),
-              "host range shares a memory page with another pinned range; pin one buffer that "
-              "holds both, or use page-aligned buffers (torch pin_memory())");
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) == hipSuccess) {
       DGS_CHECK(a.type != hipMemoryTypeHost,

@@ -196,6 +196,14 @@ __global__ __launch_bounds__(kThreads) void k_dscatter(const int64_t *a, Count n
   const int64_t na = nac.get();
   const int64_t n = na + *d_nb;
   const int64_t tile = blockIdx.x;
+  if (n == 0) {
+    // an empty call (no seeds): the count and the publication still happen, from tile 0
+    if (tile == 0 && threadIdx.x == 0) {
+      *d_nunique = 0;
+      publish_sizes(pub);
+    }
+    return;
+  }
   const int64_t ntiles = (n + kCompactTile - 1) / kCompactTile;
   if (tile >= ntiles) return;
   // this tile's offset: sum of the earlier tiles' counts (issued before the element loads)

@@ -2,6 +2,7 @@
 #include "services.h"
 
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -332,14 +333,44 @@ size_t Sampler::num_contexts() {
 // All hops are enqueued without host synchronisation: hop h+1 reads its seed count from the
 // device word the relabel of hop h wrote, grids are sized by the host-side upper bounds, and
 // the per-hop sizes are published to pinned host memory by the last kernel.
+// DGS_CALL_TRACE=1 (diagnostics): host time of the synchronous call's phases -- entry to the
+// last launch enqueued, then to the sizes seen -- averaged and printed to stderr at exit.
+namespace {
+struct CallTrace {
+  std::mutex mu;
+  int64_t n = 0;
+  double launch_us = 0, wait_us = 0;
+  ~CallTrace() {
+    if (n)
+      fprintf(stderr, "[dgs call trace] %lld synchronous calls: launches %.2f us, wait for sizes "
+              "%.2f us (host, per call)\n", (long long)n, launch_us / n, wait_us / n);
+  }
+};
+CallTrace *call_trace() {
+  // (printed by the destructor at process exit)
+  static std::unique_ptr<CallTrace> t(std::getenv("DGS_CALL_TRACE") ? new CallTrace() : nullptr);
+  return t.get();
+}
+}  // namespace
+
 void Sampler::sample(const int64_t *seeds, int64_t n_seeds, const int64_t *fan_out, int L,
                      bool replace, int64_t *const *frontiers, int64_t *const *rows,
                      int64_t *const *cols, int64_t *sizes, hipStream_t st,
                      const uint64_t *launch_seeds) {
   if (L <= 0) return;
+  CallTrace *tr = call_trace();
+  const auto t0 = std::chrono::steady_clock::now();
   sample_begin(seeds, n_seeds, fan_out, L, replace, frontiers, rows, cols, st, launch_seeds,
                /*host_async=*/false, /*solo=*/true);
+  const auto t1 = std::chrono::steady_clock::now();
   sample_end(L, sizes, st);
+  if (tr) {
+    const auto t2 = std::chrono::steady_clock::now();
+    std::lock_guard<std::mutex> g(tr->mu);
+    tr->n += 1;
+    tr->launch_us += std::chrono::duration<double, std::micro>(t1 - t0).count();
+    tr->wait_us += std::chrono::duration<double, std::micro>(t2 - t1).count();
+  }
 }
 
 // Per-context device words, at fixed offsets whatever the call's hop count: the diagnostics of

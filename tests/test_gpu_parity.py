@@ -647,8 +647,8 @@ def test_services_over_views_of_one_buffer(dgs):
 
 def test_c_abi_registration_rules(dgs):
     """At the C ABI: a range that only partly lies in a pin is refused (no unreferenced, partly
-    unmapped view), as is one that shares a memory page with a pin; an unregister must name a
-    pointer that dgs_host_register pinned, and a contained range shares the registration."""
+    unmapped view); an unregister must name a pointer that dgs_host_register pinned, and a
+    contained range shares the registration."""
     import ctypes
     from dgs._lib import lib
     buf = torch.zeros(1 << 16, dtype=torch.uint8)
@@ -664,12 +664,14 @@ def test_c_abi_registration_rules(dgs):
     # a service over such a range is refused the same way
     with pytest.raises(RuntimeError, match="overlaps"):
         _raw_feature_server(base + 1024, 256, 32)
-    # disjoint bytes, shared page: refused (a pin of [q, q + 100) and one of [q + 200, ...))
+    # disjoint bytes on one page: two registrations, as the reference's cudaHostRegister of
+    # neighbouring tensors (HIP locks the shared page for each; tests/test_host_pages_gpu.py
+    # copies through such pages)
     q = base + 3 * 4096
     assert lib.dgs_host_register(ctypes.c_void_p(q), 100) == 0
-    assert lib.dgs_host_register(ctypes.c_void_p(q + 200), 100) != 0
-    assert b"shares a memory page" in lib.dgs_last_error()
+    assert lib.dgs_host_register(ctypes.c_void_p(q + 200), 100) == 0
     assert lib.dgs_host_unregister(ctypes.c_void_p(q)) == 0
+    assert lib.dgs_host_unregister(ctypes.c_void_p(q + 200)) == 0
     # the page after the first pin is free
     assert lib.dgs_host_register(ctypes.c_void_p(base + 4096), 4096) == 0
     assert lib.dgs_host_unregister(ctypes.c_void_p(base + 4096)) == 0

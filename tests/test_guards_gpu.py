@@ -116,10 +116,10 @@ def test_loader_names_the_batch_of_a_bad_id_and_closes(dgs):
     srv = dgs.classes.P2PCacheFeatureServer(torch.randn(n, 8), torch.arange(n), 0)
     labels = torch.arange(100, dtype=torch.int64, device="cuda")
     _drain_errors(dgs)
-    seeds = [torch.tensor([1, 500, 3], device="cuda")] + \
+    seeds = [torch.tensor([1, 250, 3], device="cuda")] + \
         [torch.tensor([4, 5, 6], device="cuda")] * 3
-    free0 = len(P._FREE_STREAMS.get(torch.device("cuda", 0), []))
     loader = PrefetchLoader(sampler, seeds, [5], server=srv, labels=labels, depth=2)
+    mine = list(loader._streams)
     handed = 0
     with pytest.raises(RuntimeError, match="outside \\[0, 100\\).*batch 0\\]"):
         for _ in loader:
@@ -127,7 +127,8 @@ def test_loader_names_the_batch_of_a_bad_id_and_closes(dgs):
             torch.cuda.synchronize()  # batch 0's report is in before the next gather entry
     assert handed == 1
     assert loader._streams == [] and not loader._inflight
-    assert len(P._FREE_STREAMS.get(torch.device("cuda", 0), [])) >= free0 + 2
+    pool = P._FREE_STREAMS.get(torch.device("cuda", 0), [])
+    assert len(mine) == 2 and all(any(s is t for t in pool) for s in mine)
 
 
 def test_cache_lists_outside_the_graph_are_refused(dgs):
@@ -255,3 +256,34 @@ def test_services_never_register_pageable_memory(dgs):
         del fs
         gc.collect()
         assert dgs.ops._host_memory_state() == base
+
+
+def test_empty_seed_batch(dgs):
+    """A batch of no seeds (a train split's empty tail): every hop's frontier and COO are empty,
+    synchronously and through the loader, and the calls around it stay exact.  (Round 6: the
+    compaction published no sizes for an empty call -- 'sizes were not published'.)"""
+    from DistGNN.dataloading import PrefetchLoader
+    from oracle import oracle as O
+    ip, ix = _small_graph(800, seed=9)
+    n = ip.numel() - 1
+    sampler = dgs.classes.P2PCacheSampler(ip, ix, torch.Tensor(), torch.arange(n), 0)
+    empty = torch.empty(0, dtype=torch.int64, device="cuda")
+    for replace in (False, True):
+        blocks = sampler._CAPI_sample_node_classifiction(empty, [5, 4, 3], replace)
+        assert len(blocks) == 3
+        for _, f, r, c in blocks:
+            assert f.numel() == 0 and r.numel() == 0 and c.numel() == 0
+    seeds = [torch.tensor([3, 9, 27], device="cuda"), empty, torch.tensor([5, 1], device="cuda")]
+    dgs.ops._CAPI_set_random_seed(31)
+    ls = dgs.ops.draw_launch_seeds(9)
+    dgs.ops._CAPI_set_random_seed(31)
+    got = [b for b, _, _ in PrefetchLoader(sampler, seeds, [5, 4, 3], depth=3)]
+    for i, (s, b) in enumerate(zip(seeds, got)):
+        exp = O.node_classification_sample(s.cpu().numpy(), ip.numpy(), ix.numpy(), [5, 4, 3],
+                                           False, ls[3 * i:3 * i + 3]) if s.numel() else None
+        for h, (_, f, r, c) in enumerate(b):
+            if exp is None:
+                assert f.numel() == r.numel() == c.numel() == 0
+            else:
+                assert np.array_equal(f.cpu().numpy(), exp[h][1])
+                assert np.array_equal(c.cpu().numpy(), exp[h][3])
