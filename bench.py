@@ -694,6 +694,9 @@ def run_workload(args, dgs, dist, world, rank, local_rank, mode, share, dev_inde
         "gather_kernel_ms_per_step": prof["gather_ms"] / args.steps,
         "sample_span_ms_per_call": side["sample_span_ms"],
         "label_select_kernel_ms": side["select_ms"],
+        # the whole step against the floors of all its kernels (HBM bytes + Philox work)
+        "step_roofline": step_floor(side.pop("blocks", None), indptr, fan_out, args.bias,
+                                    args.dim, elapsed_all * 1e3 / args.steps),
         "roofline": {
             "bound": ("hbm" if world == 1 or mode == "replicated"
                       else "hbm (local rows) + xGMI (remote rows)"),
@@ -899,7 +902,7 @@ def side_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, cache
     for s in side_seeds[:3]:
         sampler._CAPI_sample_node_classifiction(s, fan_out, False)
     torch.cuda.synchronize()
-    side_nids, rates, call_ms = [], [], []
+    side_nids, rates, call_ms, side_blocks = [], [], [], []
     for s in side_seeds[3:]:
         torch.cuda.synchronize()
         tc = time.perf_counter()
@@ -909,6 +912,8 @@ def side_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, cache
         call_ms.append(dt * 1e3)
         rates.append(sum(b[2].numel() for b in blocks) / dt)
         side_nids.append(blocks[-1][1])
+        if len(side_blocks) < 8:
+            side_blocks.append(blocks)
     # GPU span of a sample call and the label select kernel (profiled, sequential)
     dgs.ops.profile_enable(dgs.ops.PROFILE_SAMPLE | dgs.ops.PROFILE_SELECT)
     for s in side_seeds[3:23]:
@@ -955,6 +960,7 @@ def side_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, cache
         torch.cuda.synchronize()
         g_rates.append(n.numel() * per_row / (time.perf_counter() - tc) / 1e9)
     return {
+        "blocks": side_blocks,
         "sequential_value": float(np.median(rates)),
         "seq_ms_median": float(np.median(call_ms)),
         "sample_span_ms": sp["sample_ms"] / max(sp["sample_calls"], 1),
@@ -967,6 +973,70 @@ def side_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, cache
         "call_gbps": float(np.median(g_rates)) if g_rates else 0.0,
         "mb_ms": mb_ms,
         "mb_gbps": (1 << 20) * per_row / (mb_ms * 1e-3) / 1e9 if mb_ms > 0 else 0.0,
+    }
+
+
+# Measured throughput floors of the two VALU-bound sampling kernels: the
+# uniform hub reservoir draws 1.15 T Philox draws/s in steady state on one huge row
+# (tools/hub_rate.py), the biased stream kernel evaluates 0.72 T hub edges/s (Philox + bound,
+# VALU active ~82 %).  A kernel cannot beat its own floor inside the pipeline either.
+UNIFORM_DRAWS_PER_S = 1.15e12
+BIAS_EDGES_PER_S = 0.72e12
+BIAS_HUB_DEG = 1024     # k_bias_boot / k_bias_stream take rows above this degree
+BIAS_BOOT_SAMPLE = 4096
+
+
+def step_floor(blocks_list, indptr, fan_out, bias, dim, ms_per_step):
+    """Step-level roofline (VERDICT r05 "Next round" 7): per batch, the SURVEY 8(d) algorithmic
+    HBM bytes of every kernel of the step at 8 TB/s (sampling per hop: 8S seeds + 16S indptr
+    pairs + 8 nnz ids + 16 nnz COO + relabel 8(S+nnz) read + 8 S' unique + 16 nnz rewrite, biased
+    + 4 sum(deg) probabilities; feature gather 2 d 4 + 8 per row; label gather 24 per seed),
+    and the Philox work of the VALU-bound kernels at their measured floors (uniform: one draw
+    per reservoir step, sum over rows of deg - k; biased: one draw per edge of every row with
+    deg > k, plus the boot's sample of the hub rows).  Averaged over the side pass's batches.
+    `sum_us` assumes no overlap between kernels; `max_us` perfect overlap of HBM and VALU work;
+    the step can be no faster than max_us."""
+    if not blocks_list:
+        return None
+    ip = indptr.numpy() if hasattr(indptr, "numpy") else indptr
+    hbm, valu, draws = [], [], []
+    for blocks in blocks_list:
+        L = len(blocks)
+        b_bytes, d = 0.0, 0.0
+        for h, (seeds, fr, r, _) in enumerate(blocks):
+            k = fan_out[L - 1 - h]
+            sd = seeds.cpu().numpy()
+            deg = (ip[sd + 1] - ip[sd]).astype(np.float64)
+            S, nnz, Sp = sd.size, r.numel(), fr.numel()
+            b_bytes += 8 * S + 16 * S + 8 * nnz + 16 * nnz + 8 * (S + nnz) + 8 * Sp + 16 * nnz
+            big = deg[deg > k]
+            if bias:
+                b_bytes += 4 * big.sum()
+                d += big.sum() + np.minimum(big[big > BIAS_HUB_DEG], BIAS_BOOT_SAMPLE).sum()
+            else:
+                d += (big - k).sum()
+        rows = blocks[-1][1].numel()
+        b_bytes += rows * (2 * dim * 4 + 8) + 24 * blocks[0][0].numel()
+        hbm.append(b_bytes)
+        draws.append(d)
+        valu.append(d / (BIAS_EDGES_PER_S if bias else UNIFORM_DRAWS_PER_S))
+    hbm_us = float(np.mean(hbm)) / (HBM_PEAK_GBPS * 1e3)
+    valu_us = float(np.mean(valu)) * 1e6
+    step_us = ms_per_step * 1e3
+    return {
+        "hbm_bytes_per_step": float(np.mean(hbm)),
+        "hbm_floor_us": hbm_us,
+        "philox_draws_per_step": float(np.mean(draws)),
+        "valu_floor_us": valu_us,
+        "valu_rate": (f"{BIAS_EDGES_PER_S / 1e12:.2f} T hub edges/s (k_bias_stream, measured)"
+                      if bias else
+                      f"{UNIFORM_DRAWS_PER_S / 1e12:.2f} T draws/s (k_hub_reservoir, measured)"),
+        "sum_us": hbm_us + valu_us,
+        "max_us": max(hbm_us, valu_us),
+        "ms_per_step": ms_per_step,
+        "frac_of_sum": (hbm_us + valu_us) / step_us if step_us > 0 else 0.0,
+        "frac_of_max": max(hbm_us, valu_us) / step_us if step_us > 0 else 0.0,
+        "batches": len(blocks_list),
     }
 
 

@@ -193,3 +193,27 @@ def test_secondary_papers_bias_record_only_for_the_default_single_gpu_run():
     assert bench.baseline_config(a2, "replicated", None).startswith("configs[3]")
     assert bench.baseline_config(bench.parse([]), "replicated", None) == "configs[1]"
     assert bench.baseline_config(bench.parse([]), "hot-shard", None) == "configs[2]"
+
+
+def test_step_floor_counts_bytes_and_draws():
+    """bench.step_floor: SURVEY 8(d) bytes per hop + gather/label bytes, and the Philox work of
+    the VALU-bound kernels (uniform: deg - k per row with deg > k; biased: deg per such row plus
+    the boot sample of rows above 1024)."""
+    import numpy as np
+    import torch
+    import bench
+    indptr = torch.tensor([0, 20, 23, 2023, 2030])  # degrees 20, 3, 2000, 7
+    seeds = torch.tensor([0, 1, 2, 3])
+    fr = torch.arange(10)
+    r = torch.zeros(12, dtype=torch.int64)
+    blocks = [(seeds, fr, r, r)]
+    f = bench.step_floor([blocks], indptr, [5], False, 4, 1.0)
+    S, nnz, Sp = 4, 12, 10
+    sample_b = 8 * S + 16 * S + 8 * nnz + 16 * nnz + 8 * (S + nnz) + 8 * Sp + 16 * nnz
+    assert f["hbm_bytes_per_step"] == sample_b + 10 * (2 * 4 * 4 + 8) + 24 * 4
+    assert f["philox_draws_per_step"] == (20 - 5) + (2000 - 5) + (7 - 5)
+    assert np.isclose(f["valu_floor_us"], f["philox_draws_per_step"] / bench.UNIFORM_DRAWS_PER_S * 1e6)
+    assert f["max_us"] == max(f["hbm_floor_us"], f["valu_floor_us"])
+    fb = bench.step_floor([blocks], indptr, [5], True, 4, 1.0)
+    assert fb["philox_draws_per_step"] == 20 + 2000 + 7 + 2000  # + boot sample of the hub row
+    assert fb["hbm_bytes_per_step"] == f["hbm_bytes_per_step"] + 4 * (20 + 2000 + 7)
