@@ -562,6 +562,25 @@ int dgs_sampler_sample_packed(dgs_sampler *s, const int64_t *seeds, int64_t n_se
   });
 }
 
+int dgs_sampler_sample_packed_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
+                                    const int64_t *fan_out, int L, int replace, int64_t *out,
+                                    void *stream) {
+  return guard([&] {
+    DGS_CHECK(L > 0 && L <= 64, "sample: 1 to 64 hops");
+    if (n_seeds > 0) check_device_cached(seeds, "seeds");
+    check_device_cached(out, "out");
+    int64_t *fr[64], *rows[64], *cols[64];
+    packed_ptrs(obj(s, "sampler"), n_seeds, fan_out, L, out, fr, rows, cols);
+    // the synchronous call's kernel shapes (solo), launched on the caller's thread
+    obj(s, "sampler").sample_begin(seeds, n_seeds, fan_out, L, replace != 0, fr, rows, cols,
+                                   S(stream), nullptr, /*host_async=*/false, /*solo=*/true);
+  });
+}
+
+int dgs_sampler_sample_wait_hop(dgs_sampler *s, int L, int h, int64_t *u_nnz, void *stream) {
+  return guard([&] { obj(s, "sampler").sample_wait_hop(L, h, u_nnz, S(stream)); });
+}
+
 int dgs_sampler_sample_begin_after(dgs_sampler *s, void *wait_for, const int64_t *seeds,
                                    int64_t n_seeds, const int64_t *fan_out, int L, int replace,
                                    int64_t *out, const uint64_t *launch_seeds, int flags,

@@ -565,9 +565,14 @@ void Sampler::launch_hops(Ctx &c, const Job &j, hipStream_t st) {
     // the last hop's scatter publishes the flag word and every size to pinned host memory (no
     // copy, no sync); each hop's count pass range-checks its sampled ids before that, so the
     // call sees its own flag
+    // Every hop's scatter publishes its (U, nnz) with the call's sequence number in the hop's
+    // S slot (host[2 + 3h], which the host never reads as a size), so a synchronous caller can
+    // build hop h's views while later hops run (sample_wait_hop); the last hop's publication
+    // then writes the flag word and every size (host[2 + 3h] back to the device word's 0).
     const bool last = h == L - 1;
     const HostSizes pub =
-        last ? HostSizes{dsz + kFlagWord, 3 * L + 1, c.sizes_host_dev, seq} : HostSizes{};
+        last ? HostSizes{dsz + kFlagWord, 3 * L + 1, c.sizes_host_dev, seq}
+             : HostSizes{dsizes + 3 * h + 1, 2, c.sizes_host_dev + 2 + 3 * h, seq};
     chk.hop = h;
     relabel_hop(cur, S, cols[h], d_nnz, nnz_cap, /*seeds_unique=*/h > 0, t, frontiers[h],
                 rows[h], cols[h], d_uniq, c.ws, st, pub, &tail, chk);
@@ -650,6 +655,39 @@ void Sampler::sample_end(int L, int64_t *sizes, hipStream_t st) {
     sizes[3 * h + 2] = hsz[2 + 3 * h + 2];
     s = sizes[3 * h + 1];
   }
+}
+
+// Waits until hop h (< L - 1) of the call outstanding on `st` has published its sizes (or the
+// whole call has), without ending the call; u_nnz = (U_h, nnz_h).
+void Sampler::sample_wait_hop(int L, int h, int64_t *u_nnz, hipStream_t st) {
+  const std::shared_ptr<Ctx> cp = ctx_find(st);
+  DGS_CHECK(cp, "sample_wait_hop: no call outstanding on this stream");
+  Ctx &c = *cp;
+  std::unique_lock<std::mutex> lk(c.mu);
+  DGS_CHECK(c.pending, "sample_wait_hop: no call outstanding on this stream");
+  DGS_CHECK(L == c.pending_L && h >= 0 && h < L, "sample_wait_hop: bad hop");
+  c.cv.wait(lk, [&] { return c.job_done; });  // an asynchronous launch has been issued
+  DGS_CHECK(!c.job_err, "sample_wait_hop: the call's launch failed (sample_end reports it)");
+  const int64_t *hsz = c.sizes_host.as<int64_t>();
+  const int64_t seq = (int64_t)c.seq;
+  for (uint64_t spin = 1;; ++spin) {
+    if (__atomic_load_n(hsz + 2 + 3 * h, __ATOMIC_ACQUIRE) == seq ||
+        __atomic_load_n(hsz, __ATOMIC_ACQUIRE) == seq)
+      break;
+    if ((spin & 255) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) {
+        DGS_CHECK(__atomic_load_n(hsz + 2 + 3 * h, __ATOMIC_ACQUIRE) == seq ||
+                      __atomic_load_n(hsz, __ATOMIC_ACQUIRE) == seq,
+                  "sample: sizes were not published");
+        break;
+      }
+      if (q != hipErrorNotReady) DGS_HIP(q);
+    }
+    __builtin_ia32_pause();
+  }
+  u_nnz[0] = hsz[3 + 3 * h];
+  u_nnz[1] = hsz[4 + 3 * h];
 }
 
 void Sampler::build_cache_rowtab(int64_t *tab, hipStream_t st) const {

@@ -91,6 +91,8 @@ class Sampler {
                     int64_t *const *cols, hipStream_t st, const uint64_t *launch_seeds,
                     bool host_async = false, bool solo = false);
   void sample_end(int L, int64_t *sizes, hipStream_t st);
+  // hop h's (U, nnz) of the call outstanding on `st`, once published (the call stays pending)
+  void sample_wait_hop(int L, int h, int64_t *u_nnz, hipStream_t st);
   // `consumer` waits for the last call ended on `st`, on the event that call recorded after its
   // launches (no event record on the caller's thread).
   void wait_ended(hipStream_t st, hipStream_t consumer);

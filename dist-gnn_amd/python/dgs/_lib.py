@@ -79,6 +79,9 @@ _SIGS = {
     "dgs_sampler_sample_begin": (c_int, [c_vp, c_vp, c_i64, p_i64, c_int, c_int, p_vp, p_vp,
                                          p_vp, ctypes.POINTER(c_u64), c_int, c_vp]),
     "dgs_sampler_sample_end": (c_int, [c_vp, c_int, p_i64, c_vp]),
+    "dgs_sampler_sample_packed_begin": (c_int, [c_vp, c_vp, c_i64, p_i64, c_int, c_int, c_vp,
+                                                c_vp]),
+    "dgs_sampler_sample_wait_hop": (c_int, [c_vp, c_int, c_int, p_i64, c_vp]),
     "dgs_sampler_sample_begin_after": (c_int, [c_vp, c_vp, c_vp, c_i64, p_i64, c_int, c_int,
                                                c_vp, ctypes.POINTER(c_u64), c_int, c_vp]),
     "dgs_loader_gather": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i64,

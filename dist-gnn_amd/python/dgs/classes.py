@@ -154,16 +154,45 @@ class P2PCacheSampler:
         return _PendingSample(self, seeds, s, L, caps, total, buf, st)
 
     def _sample(self, seeds, fan_out, replace, launch_seeds):
+        """The synchronous call: every hop enqueued at once, then each hop's views are built as
+        soon as its compaction publishes (U, nnz) -- while the later hops still run on the GPU
+        (round 6: the views no longer wait for the whole call)."""
         if launch_seeds is not None:
             return self._sample_seeded(seeds, fan_out, replace, launch_seeds)
         s, L, fo, caps, total, buf, _ = self._prepare(seeds, fan_out, packed=True)
         if L == 0:
             return []
+        st = stream_ptr(s.device)
+        h_ = self._h
+        check(lib.dgs_sampler_sample_packed_begin(h_, s.data_ptr(), s.numel(), fo, L,
+                                                  int(bool(replace)), buf.data_ptr(), st))
+        cast = self._id_dtype != torch.int64
+        out, cur, off = [], seeds, 0
+        un = (c_i64 * 2)()
+        try:
+            for h in range(L - 1):
+                check(lib.dgs_sampler_sample_wait_hop(h_, L, h, un, st))
+                f, e = caps[h]
+                U, nnz = un[0], un[1]
+                fr, r, c = (buf[off:off + U], buf[off + f:off + f + nnz],
+                            buf[off + f + e:off + f + e + nnz])
+                if cast:
+                    fr, r, c = fr.to(self._id_dtype), r.to(self._id_dtype), c.to(self._id_dtype)
+                out.append((cur, fr, r, c))
+                cur, off = fr, off + f + 2 * e
+        except BaseException:
+            sizes = (c_i64 * (3 * L))()
+            lib.dgs_sampler_sample_end(h_, L, sizes, st)  # ends the call (its error, if any,
+            raise                                         # is the one raised here)
         sizes = (c_i64 * (3 * L))()
-        check(lib.dgs_sampler_sample_packed(self._h, s.data_ptr(), s.numel(), fo, L,
-                                            int(bool(replace)), buf.data_ptr(), sizes,
-                                            stream_ptr(s.device)))
-        return self._views(seeds, buf, caps, total, sizes, L)
+        check(lib.dgs_sampler_sample_end(h_, L, sizes, st))
+        f, e = caps[L - 1]
+        U, nnz = sizes[3 * L - 2], sizes[3 * L - 1]
+        fr, r, c = buf[off:off + U], buf[off + f:off + f + nnz], buf[off + f + e:off + f + e + nnz]
+        if cast:
+            fr, r, c = fr.to(self._id_dtype), r.to(self._id_dtype), c.to(self._id_dtype)
+        out.append((cur, fr, r, c))
+        return out
 
     def _prepare(self, seeds, fan_out, packed=False, alloc_stream=None):
         """packed: no per-hop pointer arrays (the buffer goes to the C ABI whole).

@@ -242,6 +242,16 @@ int dgs_sampler_sample_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_see
                              int64_t *const *cols, const uint64_t *launch_seeds, int flags,
                              void *stream);
 int dgs_sampler_sample_end(dgs_sampler *s, int L, int64_t *sizes_out, void *stream);
+/* ADDITIVE: the synchronous call (dgs_sampler_sample_packed) in parts, so the caller can use a
+ * hop's outputs while later hops run: _packed_begin enqueues every hop with the synchronous
+ * call's kernel shapes; _wait_hop returns hop h's (U_h, nnz_h) once its compaction has published
+ * them (h < L, the call stays outstanding); dgs_sampler_sample_end ends the call (and reports
+ * its errors) as for dgs_sampler_sample_begin.  Same draws and outputs as the one-call form. */
+int dgs_sampler_sample_packed_begin(dgs_sampler *s, const int64_t *seeds, int64_t n_seeds,
+                                    const int64_t *fan_out, int L, int replace, int64_t *out,
+                                    void *stream);
+int dgs_sampler_sample_wait_hop(dgs_sampler *s, int L, int h, int64_t *u_nnz /* [2] */,
+                                void *stream);
 /* ADDITIVE: with DGS_SAMPLE_WAIT in `flags`, `stream` first waits for the work enqueued on
  * `wait_for` so far (any stream, NULL = the null stream); with DGS_SAMPLE_WAIT_EVENT it waits on
  * the event `wait_for`; a non-NULL `wait_for` without either flag is an error (round 3's
