@@ -373,7 +373,7 @@ def timed_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, dist
     gaps = np.diff(np.array([t0] + step_t)) * 1e3
     tr = getattr(it, "trace", None)
     if tr:  # DGS_PREFETCH_TRACE=1: the first steps' phases, us after t0
-        print("[bench] loader trace: " + " ".join(f"{n}@{(t - t0) * 1e6:.0f}" for n, t in tr[:16]),
+        print("[bench] loader trace: " + " ".join(f"{n}@{(t - t0) * 1e6:.0f}" for n, t in tr),
               file=sys.stderr)
     step_gaps = {"p10": float(np.percentile(gaps, 10)), "p50": float(np.median(gaps)),
                  "p90": float(np.percentile(gaps, 90)), "max": float(gaps.max())}

@@ -39,10 +39,6 @@ _HOST_ASYNC = os.environ.get("DGS_PREFETCH_SYNC", "0") != "1"
 _PRIORITY = int(os.environ.get("DGS_PREFETCH_STREAM_PRIORITY", "0"))
 # DGS_PREFETCH_TRACE=1 (diagnostics): host timestamps of each __next__'s phases in self.trace
 _TRACE = os.environ.get("DGS_PREFETCH_TRACE") == "1"
-# The first `depth` submissions of a loader are spaced DGS_PREFETCH_RAMP_US apart (host spin;
-# default 0 = off): submitted together, the first batches run in lock step and complete
-# together, late (experiments, tools/ramp_ab.sh)
-_RAMP_US = float(os.environ.get("DGS_PREFETCH_RAMP_US", "0"))
 _STREAMS_LOCK = threading.Lock()
 # (stream, buffer size) pairs whose allocator pool was given a second output buffer
 _PRIMED = set()
@@ -195,13 +191,10 @@ class PrefetchLoader:
         if _TRACE:
             self.trace.append(("next", time.perf_counter()))
         cur = self._caller_stream()
+        # (the depth batches are submitted together and run their phases in lock step: spacing
+        # the submissions -- the first ones, or every one -- measured slower at 20 and 300 steps,
+        # profiles/r06_ab_loader_pacing_rejected.txt)
         while (self._pulled or not self._exhausted) and len(self._inflight) < len(self._st):
-            if _RAMP_US > 0 and 0 < self._n < len(self._st):
-                if self._n == 1:
-                    self._t_ramp = time.perf_counter()
-                due = self._t_ramp + _RAMP_US * 1e-6 * self._n
-                while time.perf_counter() < due:
-                    pass
             self._submit(cur)
         if not self._inflight:
             self.close()  # returns the streams
