@@ -976,10 +976,14 @@ def side_pass(dgs, sampler, server, labels_dev, fan_out, args, next_seeds, cache
     }
 
 
-# Measured throughput floors of the two VALU-bound sampling kernels: the
-# uniform hub reservoir draws 1.15 T Philox draws/s in steady state on one huge row
-# (tools/hub_rate.py), the biased stream kernel evaluates 0.72 T hub edges/s (Philox + bound,
-# VALU active ~82 %).  A kernel cannot beat its own floor inside the pipeline either.
+# VALU issue floor of the two Philox-bound sampling kernels: wave64 VALU instructions per unit of
+# work (uniform hub reservoir: ~30 per 64 draws, SQ counters, profiles/r02_sampling_pmc_sq.txt;
+# biased stream: 107 per 512 hub edges -- a 256-edge chunk per half-wave),
+# issued at one wave64 instruction per 4 cycles on each of the 1024 SIMDs at 2.4 GHz.  The kernels'
+# measured steady-state rates (1.15 T draws/s, 0.72 T hub edges/s) are reported beside it.
+PEAK_WAVE_INSTR_PER_S = 1024 * 2.4e9 / 4
+UNIFORM_INSTR_PER_DRAW = 30.0 / 64.0
+BIAS_INSTR_PER_EDGE = 107.0 / 512.0
 UNIFORM_DRAWS_PER_S = 1.15e12
 BIAS_EDGES_PER_S = 0.72e12
 BIAS_HUB_DEG = 1024     # k_bias_boot / k_bias_stream take rows above this degree
@@ -991,15 +995,16 @@ def step_floor(blocks_list, indptr, fan_out, bias, dim, ms_per_step):
     HBM bytes of every kernel of the step at 8 TB/s (sampling per hop: 8S seeds + 16S indptr
     pairs + 8 nnz ids + 16 nnz COO + relabel 8(S+nnz) read + 8 S' unique + 16 nnz rewrite, biased
     + 4 sum(deg) probabilities; feature gather 2 d 4 + 8 per row; label gather 24 per seed),
-    and the Philox work of the VALU-bound kernels at their measured floors (uniform: one draw
-    per reservoir step, sum over rows of deg - k; biased: one draw per edge of every row with
+    and the Philox work of the VALU-bound kernels at the VALU issue peak (uniform: one draw per
+    reservoir step, sum over rows of deg - k; biased: one draw per edge of every row with
     deg > k, plus the boot's sample of the hub rows).  Averaged over the side pass's batches.
     `sum_us` assumes no overlap between kernels; `max_us` perfect overlap of HBM and VALU work;
-    the step can be no faster than max_us."""
+    the step can be no faster than max_us.  `valu_at_measured_rate_us`: the same work at the
+    kernels' measured steady-state rates."""
     if not blocks_list:
         return None
     ip = indptr.numpy() if hasattr(indptr, "numpy") else indptr
-    hbm, valu, draws = [], [], []
+    hbm, valu, meas, draws = [], [], [], []
     for blocks in blocks_list:
         L = len(blocks)
         b_bytes, d = 0.0, 0.0
@@ -1019,7 +1024,9 @@ def step_floor(blocks_list, indptr, fan_out, bias, dim, ms_per_step):
         b_bytes += rows * (2 * dim * 4 + 8) + 24 * blocks[0][0].numel()
         hbm.append(b_bytes)
         draws.append(d)
-        valu.append(d / (BIAS_EDGES_PER_S if bias else UNIFORM_DRAWS_PER_S))
+        valu.append(d * (BIAS_INSTR_PER_EDGE if bias else UNIFORM_INSTR_PER_DRAW) /
+                    PEAK_WAVE_INSTR_PER_S)
+        meas.append(d / (BIAS_EDGES_PER_S if bias else UNIFORM_DRAWS_PER_S))
     hbm_us = float(np.mean(hbm)) / (HBM_PEAK_GBPS * 1e3)
     valu_us = float(np.mean(valu)) * 1e6
     step_us = ms_per_step * 1e3
@@ -1028,9 +1035,12 @@ def step_floor(blocks_list, indptr, fan_out, bias, dim, ms_per_step):
         "hbm_floor_us": hbm_us,
         "philox_draws_per_step": float(np.mean(draws)),
         "valu_floor_us": valu_us,
-        "valu_rate": (f"{BIAS_EDGES_PER_S / 1e12:.2f} T hub edges/s (k_bias_stream, measured)"
-                      if bias else
-                      f"{UNIFORM_DRAWS_PER_S / 1e12:.2f} T draws/s (k_hub_reservoir, measured)"),
+        "valu_rate": (f"{BIAS_INSTR_PER_EDGE:.3f} wave64 VALU instructions per hub edge "
+                      "(k_bias_stream)" if bias else
+                      f"{UNIFORM_INSTR_PER_DRAW:.3f} wave64 VALU instructions per draw "
+                      "(k_hub_reservoir)") +
+                     f" at {PEAK_WAVE_INSTR_PER_S / 1e12:.3f} T wave64 instructions/s",
+        "valu_at_measured_rate_us": float(np.mean(meas)) * 1e6,
         "sum_us": hbm_us + valu_us,
         "max_us": max(hbm_us, valu_us),
         "ms_per_step": ms_per_step,

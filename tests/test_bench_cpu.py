@@ -212,7 +212,10 @@ def test_step_floor_counts_bytes_and_draws():
     sample_b = 8 * S + 16 * S + 8 * nnz + 16 * nnz + 8 * (S + nnz) + 8 * Sp + 16 * nnz
     assert f["hbm_bytes_per_step"] == sample_b + 10 * (2 * 4 * 4 + 8) + 24 * 4
     assert f["philox_draws_per_step"] == (20 - 5) + (2000 - 5) + (7 - 5)
-    assert np.isclose(f["valu_floor_us"], f["philox_draws_per_step"] / bench.UNIFORM_DRAWS_PER_S * 1e6)
+    assert np.isclose(f["valu_floor_us"], f["philox_draws_per_step"] * bench.UNIFORM_INSTR_PER_DRAW
+                      / bench.PEAK_WAVE_INSTR_PER_S * 1e6)
+    assert np.isclose(f["valu_at_measured_rate_us"],
+                      f["philox_draws_per_step"] / bench.UNIFORM_DRAWS_PER_S * 1e6)
     assert f["max_us"] == max(f["hbm_floor_us"], f["valu_floor_us"])
     fb = bench.step_floor([blocks], indptr, [5], True, 4, 1.0)
     assert fb["philox_draws_per_step"] == 20 + 2000 + 7 + 2000  # + boot sample of the hub row
