@@ -523,7 +523,9 @@ void Sampler::launch_hops(Ctx &c, const Job &j, hipStream_t st) {
   if (c.sizes_host.bytes < sizeof(int64_t) * (size_t)(3 * L + 2)) {
     c.sizes_host.flags = hipHostMallocCoherent | hipHostMallocMapped;
     c.sizes_host.ensure(sizeof(int64_t) * (size_t)(3 * L + 2));
-    c.sizes_host.as<int64_t>()[0] = 0;
+    // every word zeroed: the per-hop markers (host[2 + 3h]) are compared with the call's
+    // sequence number, and a recycled pinned block could hold a matching stale value
+    std::memset(c.sizes_host.p, 0, c.sizes_host.bytes);
     DGS_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.sizes_host_dev),
                                     c.sizes_host.p, 0));
   }
