@@ -105,7 +105,7 @@ def parse(argv=None):
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--seed", type=int, default=20261015)
-    p.add_argument("--setup-timeout", type=float, default=900.0,
+    p.add_argument("--setup-timeout", type=float, default=300.0,
                    help="N > 1: bound (s) of every setup / collective phase; a rank stalled "
                         "longer exits non-zero naming the phase (DistGNN.dist.SetupWatchdog)")
     p.add_argument("--secondary", choices=["auto", "none", "papers_bias"], default="auto",
