@@ -634,6 +634,17 @@ int dgs_sampler_local_cache(const dgs_sampler *s, const int64_t **sub_indptr, in
   });
 }
 
+int dgs_sampler_cache_hashmap_capacity(const dgs_sampler *s, int64_t *dir_size) {
+  return guard([&] { *dir_size = obj(s, "sampler").cache_hashmap_capacity(); });
+}
+
+int dgs_sampler_cache_hashmap_fill(const dgs_sampler *s, int id_bytes, void *key, void *idx,
+                                   void *devid, void *stream) {
+  return guard([&] {
+    obj(s, "sampler").cache_hashmap_fill(id_bytes, key, idx, devid, S(stream));
+  });
+}
+
 int dgs_sampler_cache_map_size(const dgs_sampler *s, int64_t *n) {
   return guard([&] { *n = obj(s, "sampler").cache_map_size(); });
 }

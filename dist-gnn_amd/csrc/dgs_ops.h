@@ -82,6 +82,12 @@ void ntab_assign(NodeEntry *ntab, int64_t num_nodes, const int64_t *nids,
 // location is a GPU; *d_count receives the count.  key/idx/devid may be null (count only).
 void cache_map_compact(const int64_t *tab, int64_t n, int64_t *key, int64_t *idx,
                        int64_t *devid, int64_t *d_count, hipStream_t st);
+// The reference's open-addressing cache map (hashmap.cu:15-77), for its getter: capacity
+// 2 * _UpPower(total) and a build from the ranks' cache lists inserted in `order` (hashmap.hip).
+int64_t refmap_dir_size(int64_t total);
+void refmap_build(const int64_t *const *lists, const int64_t *counts, const int *order,
+                  int nlists, int id_bytes, int64_t dir, void *key, void *idx, void *dev,
+                  hipStream_t st);
 // frontier heat (preprocess_heat.cu); fixed_acc != nullptr: deterministic fixed-point
 // accumulation in fixed_acc[num_nodes] (scratch), then written to frontier_heat as float
 void heat(const int64_t *seeds, int64_t n_seeds, const int64_t *indptr, const int64_t *indices,

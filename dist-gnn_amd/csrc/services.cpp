@@ -699,6 +699,25 @@ void Sampler::build_cache_rowtab(int64_t *tab, hipStream_t st) const {
                   st);
 }
 
+int64_t Sampler::cache_hashmap_capacity() const {
+  int64_t total = 0;
+  for (int d = 0; d < world_; ++d) total += nids_srv_->items(d);
+  return refmap_dir_size(total);
+}
+
+void Sampler::cache_hashmap_fill(int id_bytes, void *key, void *idx, void *devid,
+                                 hipStream_t st) const {
+  std::vector<const int64_t *> lists(world_);
+  std::vector<int64_t> counts(world_);
+  for (int d = 0; d < world_; ++d) {
+    lists[d] = (const int64_t *)nids_srv_->ptr(d);
+    counts[d] = nids_srv_->items(d);
+  }
+  const std::vector<int> order = rotation(rank_, world_);  // remote ranks, then the local one
+  refmap_build(lists.data(), counts.data(), order.data(), (int)order.size(), id_bytes,
+               cache_hashmap_capacity(), key, idx, devid, st);
+}
+
 int64_t Sampler::cache_map_size() const {
   int64_t n = 0;
   for (int d = 0; d < world_; ++d) n += nids_srv_->items(d);

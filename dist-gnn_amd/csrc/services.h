@@ -105,6 +105,10 @@ class Sampler {
   const float *sub_probs() const {
     return probs_srv_ ? (const float *)probs_srv_->local() : nullptr;
   }
+  // the reference's open-addressing cache map (hashmap.cu:15-77): capacity, then a build into
+  // caller buffers of that many ids (id_bytes 4 or 8)
+  int64_t cache_hashmap_capacity() const;
+  void cache_hashmap_fill(int id_bytes, void *key, void *idx, void *devid, hipStream_t st) const;
   int64_t cache_map_size() const;
   void cache_map_fill(int64_t *key, int64_t *idx, int64_t *devid, hipStream_t st) const;
 

@@ -88,6 +88,8 @@ _SIGS = {
                                   c_vp, c_i64, c_vp]),
     "dgs_sampler_context_count": (c_int, [c_vp, p_i64]),
     "dgs_sampler_local_cache": (c_int, [c_vp, p_vp, p_i64, p_vp, p_i64, p_vp]),
+    "dgs_sampler_cache_hashmap_capacity": (c_int, [c_vp, p_i64]),
+    "dgs_sampler_cache_hashmap_fill": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "dgs_sampler_cache_map_size": (c_int, [c_vp, p_i64]),
     "dgs_sampler_cache_map_fill": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "dgs_sampler_destroy": (c_int, [c_vp]),

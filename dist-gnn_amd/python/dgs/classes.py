@@ -85,6 +85,9 @@ class P2PCacheSampler:
             self._keep.append(pr)
         cn = cache_nids.to(torch.int64).contiguous()
         self._keep.append(cn)
+        # the reference's cache map holds ids of the cache list's type (hashmap.cu:18-31)
+        self._cache_dtype = cache_nids.dtype if cache_nids.dtype in (torch.int32, torch.int64) \
+            else torch.int64
         self.num_nodes = ip.numel() - 1
         h = c_vp()
         # pageable host arrays are copied by the library (never registered in place); pinned
@@ -282,9 +285,23 @@ class P2PCacheSampler:
         return sub_indptr, sub_indices, sub_probs
 
     def _CAPI_get_local_cache_hashmap_tensors(self):
-        """(key, idx, devid) of every cached node, local entries first in priority
-        (hashmap.cu:37-72).  Compact nid-ordered form: the reference's open-addressing
-        layout is an implementation detail, only the lookup semantics are kept."""
+        """sampler.cc:197-201 -> (key, idx, devid): the reference's open-addressing cache map
+        (hashmap.cu:15-77) -- 2 * _UpPower(total cached) slots of the cache lists' id type, -1
+        where empty, every rank's list inserted with the reference's Murmur3 hash and probe
+        sequence in its rotation order (local list last).  Built on the device when called."""
+        n = c_i64()
+        check(lib.dgs_sampler_cache_hashmap_capacity(self._h, ctypes.byref(n)))
+        dt = self._cache_dtype
+        key = torch.empty(n.value, dtype=dt, device=self.device)
+        idx = torch.empty(n.value, dtype=dt, device=self.device)
+        devid = torch.empty(n.value, dtype=dt, device=self.device)
+        check(lib.dgs_sampler_cache_hashmap_fill(self._h, key.element_size(), ptr(key), ptr(idx),
+                                                 ptr(devid), stream_ptr(self.device)))
+        return key, idx, devid
+
+    def _local_cache_map_compact(self):
+        """ADDITIVE: (key, idx, devid) with one entry per cached node, in node-id order, local
+        entries taking priority (the lookup results of the map above, int64)."""
         n = c_i64()
         check(lib.dgs_sampler_cache_map_size(self._h, ctypes.byref(n)))
         key = torch.empty(n.value, dtype=torch.int64, device=self.device)

@@ -272,12 +272,19 @@ int dgs_sampler_context_count(dgs_sampler *s, int64_t *n);
 int dgs_sampler_local_cache(const dgs_sampler *s, const int64_t **sub_indptr, int64_t *n_rows,
                             const int64_t **sub_indices, int64_t *n_edges,
                             const float **sub_probs);
-/* _CAPI_get_local_cache_hashmap_tensors (sampler.cc:197-201): the (nid, row, device) map of
- * every cached node, local entries taking priority (hashmap.cu:37-72).  Two-step: query
- * the count, then fill caller buffers (device).  SHAPE DEVIATION: the reference returns its
- * open-addressing table arrays (capacity 2 * UpPow(total cached), empty slots included,
- * hashmap.cu:20, sampler.cc:192-196); this returns one entry per cached node, in node-id order,
- * no empty slots -- the same lookup results. */
+/* _CAPI_get_local_cache_hashmap_tensors (sampler.cc:197-201): the reference's open-addressing
+ * cache map (hashmap.cu:15-77) -- key / idx / devid arrays of dir_size = 2 * _UpPower(total cached)
+ * ids of `id_bytes` (4 or 8, the cache lists' id type), empty slots -1, every rank's list inserted
+ * in the reference's rotation order with its Murmur3 hash and probe sequence, the local list last
+ * (a node cached locally keeps its local idx/devid).  Built on the device when asked for (SYNC);
+ * the sampler's lookups use its dense node table instead.  As in the reference, the slot a key
+ * lands in depends on the order of concurrent inserts; the key set and every lookup do not. */
+int dgs_sampler_cache_hashmap_capacity(const dgs_sampler *s, int64_t *dir_size);
+int dgs_sampler_cache_hashmap_fill(const dgs_sampler *s, int id_bytes, void *key, void *idx,
+                                   void *devid, void *stream);
+/* ADDITIVE: the same map compacted -- one (nid, row, device) entry per cached node, in node-id
+ * order, local entries taking priority.  Two-step: the count, then a fill of caller buffers
+ * (device, int64). */
 int dgs_sampler_cache_map_size(const dgs_sampler *s, int64_t *n);
 int dgs_sampler_cache_map_fill(const dgs_sampler *s, int64_t *key, int64_t *idx,
                                int64_t *devid, void *stream);

@@ -266,3 +266,84 @@ def frontier_heat(seeds, indptr, indices, seeds_heat, num_picks, indptr_diff=0, 
 
 def max_threads():
     return lib().oracle_max_threads()
+
+
+# ------------------------------------------------------------------ the reference's cache map
+_M32 = 0xFFFFFFFF
+_M64 = 0xFFFFFFFFFFFFFFFF
+
+
+def _murmur32(k):
+    """hashmap.h:52-59 (Hash32Shift)."""
+    k &= _M32
+    k ^= k >> 16
+    k = (k * 0x85EBCA6B) & _M32
+    k ^= k >> 13
+    k = (k * 0xC2B2AE35) & _M32
+    k ^= k >> 16
+    return k
+
+
+def _murmur64(k):
+    """hashmap.h:62-69 (Hash64Shift)."""
+    k &= _M64
+    k ^= k >> 33
+    k = (k * 0xFF51AFD7ED558CCD) & _M64
+    k ^= k >> 33
+    k = (k * 0xC4CEB9FE1A85EC53) & _M64
+    k ^= k >> 33
+    return k
+
+
+def cache_hashmap_dir_size(total):
+    """hashmap.cu:18 dir_size = _UpPower(total) * 2; _UpPower = 1 << (uint32)(log2(key) + 1),
+    hashmap.h:91-94."""
+    import math
+    return (1 << int(math.log2(total) + 1)) * 2
+
+
+def _home(key, cap, id_bytes):
+    """hashmap.h:71-85: hash(int64 key) = (uint32)Hash64Shift(key) & (cap-1); int32: Hash32."""
+    return (_murmur64(key) & _M32 if id_bytes == 8 else _murmur32(key)) & (cap - 1)
+
+
+def cache_hashmap(lists, local_rank, id_bytes=8):
+    """CreateNidsP2PCacheHashMapCUDA (hashmap.cu:15-77) executed sequentially: the remote ranks'
+    lists in rotation order (index = (d + local_rank) % W), then the local list; each key by
+    Hashmap::Update (hashmap.h:17-31: CAS at hash(key), then pos <- hash(pos + delta),
+    delta = 1, 2, ..., value and device id written at the slot it holds).  Returns (key, idx,
+    devid) int64 arrays of dir_size, -1 where empty.  (The reference inserts a list's keys
+    concurrently: where two keys' probe chains meet, the slot each ends in depends on that
+    order; this is the layout of one order, list order.)"""
+    W = len(lists)
+    total = sum(len(x) for x in lists)
+    cap = cache_hashmap_dir_size(total)
+    key = np.full(cap, -1, np.int64)
+    idx = np.full(cap, -1, np.int64)
+    dev = np.full(cap, -1, np.int64)
+    order = [(d + local_rank) % W for d in range(W)]
+    order = [i for i in order if i != local_rank] + [local_rank]
+    for d in order:
+        for i, k in enumerate(np.asarray(lists[d], np.int64).tolist()):
+            pos, delta = _home(k, cap, id_bytes), 1
+            while key[pos] != k and key[pos] != -1:
+                pos = _murmur32(pos + delta) & (cap - 1)
+                delta += 1
+            key[pos] = k
+            idx[pos] = i
+            dev[pos] = d
+    return key, idx, dev
+
+
+def cache_hashmap_find(key, k, id_bytes=8):
+    """Hashmap::SearchForPos (hashmap.h:33-47): the slot holding k, or -1."""
+    cap = len(key)
+    pos, delta = _home(int(k), cap, id_bytes), 1
+    for _ in range(4 * cap):
+        if key[pos] == k:
+            return pos
+        if key[pos] == -1:
+            return -1
+        pos = _murmur32(pos + delta) & (cap - 1)
+        delta += 1
+    return -1

@@ -56,8 +56,10 @@ def main(out_path):
         res[f"sample_bias{int(bias)}"] = {
             "seeds": seeds.tolist(),
             "hops": [[f.tolist(), r.tolist(), c.tolist()] for (_, f, r, c) in out]}
-        key, idx, devid = s._CAPI_get_local_cache_hashmap_tensors()
+        key, idx, devid = s._local_cache_map_compact()
         res[f"map_bias{int(bias)}"] = [key.tolist(), idx.tolist(), devid.tolist()]
+        key, idx, devid = s._CAPI_get_local_cache_hashmap_tensors()
+        res[f"refmap_bias{int(bias)}"] = [key.tolist(), idx.tolist(), devid.tolist()]
         del s
     data = rng.standard_normal((n, 33)).astype(np.float32)
     fs2 = dgs.classes.P2PCacheFeatureServer(torch.from_numpy(data), torch.from_numpy(mine), 0)

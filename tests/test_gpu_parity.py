@@ -357,11 +357,47 @@ def test_sampler_getters(dgs):
     si, sx, sp = s._CAPI_get_local_cache_structure_tensors()
     assert si.tolist() == [0, 4, 4] and sx.tolist() == [1, 2, 3, 4]
     assert torch.allclose(sp.cpu(), torch.tensor([0.1, 0.2, 0.3, 0.4]))
-    key, idx, devid = s._CAPI_get_local_cache_hashmap_tensors()
+    key, idx, devid = s._local_cache_map_compact()
     assert key.tolist() == [0, 3] and idx.tolist() == [0, 1] and devid.tolist() == [0, 0]
+    # the reference's own layout (hashmap.cu:15-77): 2 * _UpPower(2) = 8 slots; two keys on
+    # distinct home slots land there, so it equals the sequential restatement slot for slot
+    key, idx, devid = s._CAPI_get_local_cache_hashmap_tensors()
+    ek, ei, ed = O.cache_hashmap([np.array([0, 3])], 0)
+    assert key.dtype == torch.int64 and len(key) == 8
+    assert key.tolist() == ek.tolist() and idx.tolist() == ei.tolist()
+    assert devid.tolist() == ed.tolist()
     # reference test_sampler_bias.py: seeds [0, 3, 5], fan-out [2, 2]
     res = s._CAPI_sample_node_classifiction(torch.tensor([0, 3, 5]).cuda(), [2, 2], False)
     assert res[0][1][:3].tolist() == [0, 3, 5]
+
+
+@pytest.mark.parametrize("id_dtype", [torch.int64, torch.int32])
+def test_reference_cache_hashmap(dgs, id_dtype):
+    """_CAPI_get_local_cache_hashmap_tensors returns the reference's open-addressing map
+    (hashmap.cu:15-77) in the cache list's id type: capacity 2 * _UpPower(n), key set, -1 where
+    empty, and every cached node's (idx, devid) reached by the reference's probe sequence;
+    a list with no colliding home slots lands slot for slot where the restatement puts it."""
+    rng = np.random.default_rng(12)
+    n = 20000
+    ip = torch.from_numpy(np.arange(0, 2 * n + 1, 2, dtype=np.int64))
+    ix = torch.from_numpy(rng.integers(0, n, 2 * n).astype(np.int64))
+    ib = 8 if id_dtype == torch.int64 else 4
+    for cache in (rng.choice(n, 5000, replace=False), np.array([17, 4, 9999])):
+        s = dgs.classes.P2PCacheSampler(ip, ix, torch.Tensor(),
+                                        torch.from_numpy(cache).to(id_dtype), 0)
+        key, idx, devid = s._CAPI_get_local_cache_hashmap_tensors()
+        assert key.dtype == id_dtype and idx.dtype == id_dtype
+        key, idx, devid = (t.cpu().numpy().astype(np.int64) for t in (key, idx, devid))
+        assert len(key) == O.cache_hashmap_dir_size(cache.size)
+        assert sorted(key[key >= 0].tolist()) == sorted(cache.tolist())
+        assert (idx[key < 0] == -1).all() and (devid[key < 0] == -1).all()
+        for i, v in enumerate(cache.tolist()):
+            pos = O.cache_hashmap_find(key, v, ib)
+            assert pos >= 0 and idx[pos] == i and devid[pos] == 0
+        ek, ei, ed = O.cache_hashmap([cache], 0, ib)
+        homes = [O._home(int(v), len(ek), ib) for v in cache.tolist()]
+        if len(set(homes)) == len(homes):
+            assert key.tolist() == ek.tolist() and idx.tolist() == ei.tolist()
 
 
 def test_feature_server_matches_oracle(dgs):

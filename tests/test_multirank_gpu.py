@@ -85,6 +85,20 @@ def test_cache_map_local_priority(results):
         assert idx == [v // 2 for v in range(600)]
 
 
+def test_reference_cache_hashmap_layout(results):
+    """_CAPI_get_local_cache_hashmap_tensors: the reference's open-addressing map built from
+    both ranks' lists (hashmap.cu:15-77): capacity 2 * _UpPower(600), the key set, and every
+    node's (idx, devid) reached by the reference's probe sequence (SearchForPos)."""
+    for r, res in enumerate(results):
+        key, idx, devid = (np.array(a) for a in res["refmap_bias0"])
+        assert len(key) == O.cache_hashmap_dir_size(600) == 2048
+        assert sorted(key[key >= 0].tolist()) == list(range(600))
+        assert (idx[key < 0] == -1).all() and (devid[key < 0] == -1).all()
+        for v in range(600):
+            pos = O.cache_hashmap_find(key, v)
+            assert pos >= 0 and idx[pos] == v // 2 and devid[pos] == v % 2
+
+
 def test_sharded_gather(results):
     assert all(res["gather_ok"] for res in results)
     # v mod 2 shard -> strided layout (peer rows through the IPC-mapped block, no table)

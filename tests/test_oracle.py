@@ -391,3 +391,32 @@ def test_heat_semantics():
         for i in range(b, e):
             exp[indices[i]] += min(1.0, heat[s] * 5 * (probs[i] / ps))
     np.testing.assert_allclose(fb, exp, rtol=1e-5)
+
+
+def test_cache_hashmap_restatement():
+    """The reference's cache map (hashmap.h / hashmap.cu:15-77), sequential: capacity
+    2 * _UpPower(total), every key found by SearchForPos, the local list's (idx, devid) win
+    for a node cached on several ranks, the key set is the union of the lists."""
+    import numpy as np
+    from oracle import oracle as O
+    assert [O.cache_hashmap_dir_size(t) for t in (1, 2, 3, 4, 5, 1000, 1024)] == \
+        [4, 8, 8, 16, 16, 2048, 4096]
+    # Murmur3 finalisers: fmix32 / fmix64 of 1 (published constants of the reference)
+    assert O._murmur32(1) == 0x514E28B7
+    assert O._murmur64(1) == 0xB456BCFC34C2CB2C
+    rng = np.random.default_rng(3)
+    for id_bytes in (8, 4):
+        lists = [rng.choice(5000, 300, replace=False) for _ in range(3)]
+        key, idx, dev = O.cache_hashmap(lists, local_rank=1, id_bytes=id_bytes)
+        assert len(key) == O.cache_hashmap_dir_size(900)
+        assert set(key[key >= 0].tolist()) == set(np.concatenate(lists).tolist())
+        # the last list in insertion order (remote 2, 0 rotation from rank 1, then local 1)
+        # holding a key writes its (idx, devid)
+        want = {}
+        for d in (2, 0, 1):
+            for i, k in enumerate(lists[d].tolist()):
+                want[k] = (i, d)
+        for k, (i, d) in want.items():
+            pos = O.cache_hashmap_find(key, k, id_bytes)
+            assert pos >= 0 and key[pos] == k
+            assert (idx[pos], dev[pos]) == (i, d)
