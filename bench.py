@@ -263,8 +263,9 @@ def hot_set(indices, N, frac, dev):
 
 
 def verify_setup(sampler, server, indices, feats, s_cache, f_cache, N, dev):
-    """The HBM copies the services made from the host inputs (read by the GPU through the
-    registered host pages) equal the inputs as torch copies them: the sampler's cached
+    """The HBM copies the services made from the host inputs (uploaded through the library's
+    pinned staging, or read through pinned host pages) equal the inputs as torch copies them:
+    the sampler's cached
     neighbour ids (when it caches every row in id order) and the feature server's cached rows.
     A mismatch ends the run before anything is timed."""
     _, sub_indices, _ = sampler._CAPI_get_local_cache_structure_tensors()
