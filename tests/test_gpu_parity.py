@@ -507,6 +507,38 @@ def test_rmat_scale16_sampler_bit_exact(dgs):
         assert np.array_equal(gc.cpu().numpy(), ec)
 
 
+@pytest.mark.parametrize("n_seeds,k,replace,dup", [
+    (1365, 5, False, False),   # S + S k = 8190 elements of cat(seeds, col): 8 compaction tiles
+    (1366, 5, False, False),   # 8196: a ninth, nearly empty tile
+    (2048, 3, False, True),    # exactly 8192, repeated seeds: rows checked and relabelled
+    (2048, 3, True, True),
+    (1200, 5, True, False),
+    (1, 7, False, False),      # one row: one sampling workgroup, one tile
+])
+def test_fused_hop_compaction_boundary(dgs, n_seeds, k, replace, dup):
+    """First hops at the tile boundaries of the compaction (k_dcount / k_dscatter, 1024-element
+    tiles) and at the 8192-element limit of the rejected fused-compaction variant
+    (profiles/r06_ab_fused_compaction_rejected.txt): bit-exact with the oracle, twice in a row
+    (the tables' clean-up), and the second hop over the first hop's frontier."""
+    from DistGNN.dataloading.synthetic import rmat_csc_numpy
+    indptr, indices = rmat_csc_numpy(14, 12, seed=31)
+    n = indptr.size - 1
+    sampler = dgs.classes.P2PCacheSampler(torch.from_numpy(indptr), torch.from_numpy(indices),
+                                          torch.Tensor(), torch.arange(n), 0)
+    rng = np.random.default_rng(n_seeds + k)
+    seeds = rng.integers(0, n, n_seeds) if dup else rng.permutation(n)[:n_seeds]
+    fan_out = [4, k]
+    for rep in range(2):  # the workgroup counter is reset by the launch that used it
+        dgs.ops._CAPI_set_random_seed(77 + rep)
+        got = sampler._CAPI_sample_node_classifiction(_cuda(seeds), fan_out, replace)
+        exp = O.node_classification_sample(seeds, indptr, indices, fan_out, replace,
+                                           O.launch_seeds(77 + rep, 2))
+        for (gs, gf, gr, gc), (es, ef, er, ec) in zip(got, exp):
+            assert np.array_equal(gf.cpu().numpy(), ef)
+            assert np.array_equal(gr.cpu().numpy(), er)
+            assert np.array_equal(gc.cpu().numpy(), ec)
+
+
 @pytest.mark.parametrize("fan_out,replace", [([15, 10, 5], False), ([25, 10], False),
                                              ([8, 4, 2], True)])
 def test_rmat_biased_multihop_bit_exact(dgs, fan_out, replace):
