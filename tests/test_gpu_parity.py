@@ -515,7 +515,7 @@ def test_rmat_scale16_sampler_bit_exact(dgs):
     (1200, 5, True, False),
     (1, 7, False, False),      # one row: one sampling workgroup, one tile
 ])
-def test_fused_hop_compaction_boundary(dgs, n_seeds, k, replace, dup):
+def test_first_hop_compaction_tile_boundary(dgs, n_seeds, k, replace, dup):
     """First hops at the tile boundaries of the compaction (k_dcount / k_dscatter, 1024-element
     tiles) and at the 8192-element limit of the rejected fused-compaction variant
     (profiles/r06_ab_fused_compaction_rejected.txt): bit-exact with the oracle, twice in a row
