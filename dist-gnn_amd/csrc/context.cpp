@@ -373,17 +373,16 @@ void upload_pageable(void *dst, const void *src, size_t bytes, hipStream_t st) {
     if (!S.buf[i]) DGS_HIP(hipHostMalloc(&S.buf[i], kStageBytes, hipHostMallocDefault));
     if (!S.done[i]) DGS_HIP(hipEventCreateWithFlags(&S.done[i], hipEventDisableTiming));
   }
-  // chunk c: wait until the DMA that last read staging buffer c & 1 is done, fill it on the
+  // chunk c: wait until the DMA that last read staging buffer c & 1 is done (this call's, or an
+  // earlier call's that ended in an error before its closing synchronisation), fill it on the
   // host, enqueue its copy (the host fills the other buffer while the DMA runs)
-  bool used[2] = {false, false};
   for (size_t off = 0, c = 0; off < bytes; off += kStageBytes, ++c) {
     const int b = (int)(c & 1);
     const size_t n = std::min(kStageBytes, bytes - off);
-    if (used[b]) DGS_HIP(hipEventSynchronize(S.done[b]));
+    DGS_HIP(hipEventSynchronize(S.done[b]));  // (an event never recorded is complete)
     host_copy(S.buf[b], (const char *)src + off, n);
     DGS_HIP(hipMemcpyAsync((char *)dst + off, S.buf[b], n, hipMemcpyHostToDevice, st));
     DGS_HIP(hipEventRecord(S.done[b], st));
-    used[b] = true;
   }
   DGS_HIP(hipStreamSynchronize(st));
 }
