@@ -489,6 +489,71 @@ def test_heat_uva_host_graph(dgs):
     dgs.ops._CAPI_tensor_unpin_memory(ix)
 
 
+# ------------------------------------------------------------------ degree boundaries
+def _degree_graph(degs, seed):
+    """Rows of exactly the given degrees (random neighbour ids) and random probabilities with
+    some zeros."""
+    rng = np.random.default_rng(seed)
+    degs = np.asarray(degs, dtype=np.int64)
+    indptr = np.concatenate([[0], np.cumsum(degs)]).astype(np.int64)
+    indices = rng.integers(0, degs.size, int(indptr[-1])).astype(np.int64)
+    probs = (rng.random(indices.size) + 0.01).astype(np.float32)
+    probs[::29] = 0.0
+    return indptr, indices, probs
+
+
+def _uniform_boundary_degrees(k, huge):
+    """Every degree class of the uniform sampler (csrc/sample.hip) around its limits: copy
+    (deg <= k), row reservoir (deg - k <= kHubT = 128), hub chunks of 512 edges, and the hub
+    chunks' modulo forms -- mod_mid below d = 8192 (24-bit product from d = 257), mod_big from
+    d = 4096 (24-bit product below 2^24) and the generic % in between."""
+    d = [0, 1, k - 1, k, k + 1, k + 127, k + 128, k + 129, k + 130, k + 128 + 512,
+         k + 129 + 512, k + 129 + 1024, 256, 257, 258, 768, 769, 4095, 4096, 4097, k + 4096,
+         k + 4097, 7680, 7681, 8192, 8193, k + 8192, k + 8193, 8704, 12345, 65537]
+    if huge:
+        d += [(1 << 24) - 200, (1 << 24) + 700]  # chunks on both sides of 2^24
+    return sorted({x for x in d if x >= 0})
+
+
+@pytest.mark.parametrize("k,replace,huge", [(1, False, False), (5, False, True),
+                                            (15, False, False), (100, False, False),
+                                            (129, False, False), (15, True, False),
+                                            (64, True, True)])
+def test_uniform_degree_boundaries(dgs, k, replace, huge):
+    """Rows at every degree limit of the uniform sampler, each sampled once and again as a
+    repeated seed, bit-exact with the oracle for two launch seeds."""
+    indptr, indices, _ = _degree_graph(_uniform_boundary_degrees(k, huge), 17 + k)
+    n = indptr.size - 1
+    seeds = np.concatenate([np.arange(n), np.arange(n)[::-3]])
+    ip, ix = _cuda(indptr), _cuda(indices)
+    for s in (1, 2):
+        dgs.ops._CAPI_set_random_seed(5000 + 10 * k + s)
+        ls = O.launch_seeds(5000 + 10 * k + s, 1)[0]
+        row, col = dgs.ops._CAPI_cuda_sample_neighbors(_cuda(seeds), ip, ix, k, replace)
+        er, ec = O.sample_uniform(seeds, indptr, indices, k, replace, ls)
+        assert np.array_equal(row.cpu().numpy(), er)
+        assert np.array_equal(col.cpu().numpy(), ec)
+
+
+@pytest.mark.parametrize("k,replace", [(1, False), (16, False), (32, False), (8, True)])
+def test_bias_degree_boundaries(dgs, k, replace):
+    """Rows around the biased sampler's limits: deg <= k, the hub limit (deg > kBiasHubT =
+    1024), whole 256-edge stream chunks and one edge past them, the boot sample's 4096 edges,
+    and a long row."""
+    degs = [0, 1, k - 1, k, k + 1, 33, 64, 65, 1023, 1024, 1025, 1280, 1281, 2047, 2048, 2049,
+            4095, 4096, 4097, 4352, 4353, 8191, 8193, 65536, 1 << 20]
+    indptr, indices, probs = _degree_graph(sorted({d for d in degs if d >= 0}), 3 + k)
+    n = indptr.size - 1
+    seeds = np.concatenate([np.arange(n), np.arange(n)[::-2]])
+    dgs.ops._CAPI_set_random_seed(7000 + k)
+    ls = O.launch_seeds(7000 + k, 1)[0]
+    row, col = dgs.ops._CAPI_cuda_sample_neighbors_bias(_cuda(seeds), _cuda(indptr),
+                                                        _cuda(indices), _cuda(probs), k, replace)
+    er, ec = O.sample_bias(seeds, indptr, indices, probs, k, replace, ls)
+    assert np.array_equal(row.cpu().numpy(), er)
+    assert np.array_equal(col.cpu().numpy(), ec)
+
+
 # ------------------------------------------------------------------ larger graph
 def test_rmat_scale16_sampler_bit_exact(dgs):
     from DistGNN.dataloading.synthetic import rmat_csc_numpy
