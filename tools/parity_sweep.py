@@ -1,0 +1,107 @@
+"""Randomised parity sweep of the node-classification sampler (GPU) against the oracle: random
+RMAT graphs (scale 8 to --max-scale, edge factor 1-24) with planted hub rows, random cache
+subsets (all, a fraction, one node), 1-3 hops of random fan-outs, with / without replacement,
+uniform or weighted (degree weights or random weights with zeros), random seed batches with
+repeats.  Every output tensor of every hop is compared exactly; a mismatch prints its
+configuration.
+
+    python tools/parity_sweep.py [--cases 300] [--seconds 240] [--seed 1] [--max-scale 14]
+        [--max-batch 2048]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "dist-gnn_amd", "python"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def graph(rng, max_scale=14):
+    from DistGNN.dataloading.synthetic import degree_probs, rmat_csc_numpy
+    scale = int(rng.integers(8, max_scale + 1))
+    ef = int(rng.integers(1, 25))
+    indptr, indices = rmat_csc_numpy(scale, ef, seed=int(rng.integers(1 << 30)))
+    n = indptr.size - 1
+    # planted hub rows (appended): degrees around the samplers' limits and a few long rows
+    extra = rng.choice([130, 144, 700, 1025, 2049, 4097, 8193, 30000], int(rng.integers(0, 4)))
+    if extra.size:
+        tails = [rng.integers(0, n, int(d)) for d in extra]
+        indptr = np.concatenate([indptr, indptr[-1] + np.cumsum([t.size for t in tails])])
+        indices = np.concatenate([indices] + tails)
+    indptr = indptr.astype(np.int64)
+    indices = indices.astype(np.int64)
+    if rng.random() < 0.5:
+        probs = degree_probs(indptr, indices)
+    else:
+        probs = (rng.random(indices.size) + 0.01).astype(np.float32)
+        probs[rng.random(indices.size) < 0.05] = 0.0
+    return indptr, indices, probs, scale, ef, extra.tolist()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", type=int, default=300)
+    ap.add_argument("--seconds", type=float, default=240.0)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--max-scale", type=int, default=14)
+    ap.add_argument("--max-batch", type=int, default=2048)
+    a = ap.parse_args()
+    import dgs
+    from oracle import oracle as O
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(a.seed)
+    t0 = time.time()
+    done = bad = 0
+    counts = {"bias": 0, "replace": 0, "hops": [0, 0, 0]}
+    while done < a.cases and time.time() - t0 < a.seconds:
+        indptr, indices, probs, scale, ef, extra = graph(rng, a.max_scale)
+        n = indptr.size - 1
+        bias = bool(rng.random() < 0.4)
+        replace = bool(rng.random() < 0.3)
+        L = int(rng.integers(1, 4))
+        kmax = 32 if bias else 40
+        fan_out = [int(rng.integers(1, kmax + 1)) for _ in range(L)]
+        c = rng.random()
+        if c < 0.4:
+            cache = np.arange(n)
+        elif c < 0.8:
+            cache = rng.permutation(n)[: max(1, int(n * rng.random()))]
+        else:
+            cache = np.array([int(rng.integers(n))])
+        B = int(rng.integers(1, a.max_batch + 1))
+        seeds = rng.integers(0, n, B) if rng.random() < 0.5 else rng.permutation(n)[: min(B, n)]
+        ls = int(rng.integers(1, 1 << 40))
+        cfg = dict(scale=scale, ef=ef, extra=extra, bias=bias, replace=replace, fan_out=fan_out,
+                   cache=int(cache.size), n=n, seeds=int(seeds.size), seed=ls)
+        s = dgs.classes.P2PCacheSampler(torch.from_numpy(indptr), torch.from_numpy(indices),
+                                        torch.from_numpy(probs) if bias else torch.Tensor(),
+                                        torch.from_numpy(cache), 0)
+        dgs.ops._CAPI_set_random_seed(ls)
+        got = s._CAPI_sample_node_classifiction(torch.from_numpy(seeds).cuda(), fan_out, replace)
+        exp = O.node_classification_sample(seeds, indptr, indices, fan_out, replace,
+                                           O.launch_seeds(ls, L), probs=probs if bias else None)
+        ok = len(got) == len(exp) and all(
+            np.array_equal(g.cpu().numpy(), e) for gh, eh in zip(got, exp) for g, e in zip(gh, eh))
+        del s
+        done += 1
+        counts["bias"] += bias
+        counts["replace"] += replace
+        counts["hops"][L - 1] += 1
+        if not ok:
+            bad += 1
+            print(f"MISMATCH {cfg}", flush=True)
+        if done % 20 == 0:
+            print(f"[sweep] {done} cases, {bad} mismatches, {time.time() - t0:.0f} s", flush=True)
+    dgs.ops._check_async_errors()
+    print(f"parity sweep: {done} cases ({counts['bias']} weighted, {counts['replace']} with "
+          f"replacement, 1/2/3 hops {counts['hops']}), {bad} mismatches, seed {a.seed}, "
+          f"{time.time() - t0:.0f} s")
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
