@@ -42,6 +42,40 @@ def graph(rng, max_scale=14):
     return indptr, indices, probs, scale, ef, extra.tolist()
 
 
+def same(got, exp):
+    return len(got) == len(exp) and all(
+        np.array_equal(g.cpu().numpy(), e) for gh, eh in zip(got, exp) for g, e in zip(gh, eh))
+
+
+def loader_case(dgs, O, rng, sampler, indptr, indices, probs, fan_out, replace, seeds, ls, cfg):
+    """2-6 batches of the configuration's seeds through PrefetchLoader (random depth, a feature
+    server over a random cache and row width): blocks against the oracle with the engine's launch
+    seeds in submission order (L per batch), features against a host index."""
+    from DistGNN.dataloading import PrefetchLoader
+    n = indptr.size - 1
+    L = len(fan_out)
+    d = int(rng.choice([1, 3, 16, 100]))
+    feats = rng.standard_normal((n, d)).astype(np.float32)
+    fcache = np.arange(n) if rng.random() < 0.5 else rng.permutation(n)[: max(1, n // 3)]
+    server = dgs.classes.P2PCacheFeatureServer(torch.from_numpy(feats), torch.from_numpy(fcache),
+                                               0)
+    nb = int(rng.integers(2, 7))
+    depth = int(rng.integers(1, 4))
+    batches = [torch.from_numpy(np.roll(seeds, 7 * i)).cuda() for i in range(nb)]
+    cfg.update(loader_batches=nb, depth=depth, dim=d, feat_cache=int(fcache.size))
+    got = list(PrefetchLoader(sampler, batches, fan_out, replace=replace, server=server,
+                              depth=depth))
+    allseeds = O.launch_seeds(ls, L * nb)
+    ok = len(got) == nb
+    for i, (b, (blocks, x, _)) in enumerate(zip(batches, got)):
+        exp = O.node_classification_sample(b.cpu().numpy(), indptr, indices, fan_out, replace,
+                                           allseeds[L * i:L * (i + 1)], probs=probs)
+        ok = ok and same(blocks, exp)
+        ok = ok and np.array_equal(x.cpu().numpy(), feats[exp[-1][1]])
+    del server
+    return ok
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=300)
@@ -49,6 +83,9 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--max-scale", type=int, default=14)
     ap.add_argument("--max-batch", type=int, default=2048)
+    ap.add_argument("--loader", action="store_true",
+                    help="run 2-6 batches per configuration through PrefetchLoader (depth 1-3) "
+                         "with a feature server, and check the features too")
     a = ap.parse_args()
     import dgs
     from oracle import oracle as O
@@ -81,11 +118,16 @@ def main():
                                         torch.from_numpy(probs) if bias else torch.Tensor(),
                                         torch.from_numpy(cache), 0)
         dgs.ops._CAPI_set_random_seed(ls)
-        got = s._CAPI_sample_node_classifiction(torch.from_numpy(seeds).cuda(), fan_out, replace)
-        exp = O.node_classification_sample(seeds, indptr, indices, fan_out, replace,
-                                           O.launch_seeds(ls, L), probs=probs if bias else None)
-        ok = len(got) == len(exp) and all(
-            np.array_equal(g.cpu().numpy(), e) for gh, eh in zip(got, exp) for g, e in zip(gh, eh))
+        if a.loader:
+            ok = loader_case(dgs, O, rng, s, indptr, indices, probs if bias else None, fan_out,
+                             replace, seeds, ls, cfg)
+        else:
+            got = s._CAPI_sample_node_classifiction(torch.from_numpy(seeds).cuda(), fan_out,
+                                                    replace)
+            exp = O.node_classification_sample(seeds, indptr, indices, fan_out, replace,
+                                               O.launch_seeds(ls, L),
+                                               probs=probs if bias else None)
+            ok = same(got, exp)
         del s
         done += 1
         counts["bias"] += bias
