@@ -76,6 +76,63 @@ def loader_case(dgs, O, rng, sampler, indptr, indices, probs, fan_out, replace, 
     return ok
 
 
+def ops_case(dgs, O, rng, max_scale):
+    """One random case of each standalone op."""
+    indptr, indices, probs, scale, ef, extra = graph(rng, max_scale)
+    n = indptr.size - 1
+    idt = torch.int32 if rng.random() < 0.4 else torch.int64
+    k = int(rng.integers(1, 41))
+    replace = bool(rng.random() < 0.3)
+    bias = bool(rng.random() < 0.4)
+    if bias:
+        k = min(k, 32)
+    seeds = rng.integers(0, n, int(rng.integers(1, 3000)))
+    ls = int(rng.integers(1, 1 << 40))
+    cfg = dict(op="sample", scale=scale, ef=ef, extra=extra, ids=str(idt), k=k, replace=replace,
+               bias=bias, seeds=int(seeds.size), seed=ls)
+    dev = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(idt).cuda()  # noqa: E731
+    dgs.ops._CAPI_set_random_seed(ls)
+    l0 = O.launch_seeds(ls, 1)[0]
+    if bias:
+        row, col = dgs.ops._CAPI_cuda_sample_neighbors_bias(
+            dev(seeds), dev(indptr), dev(indices), torch.from_numpy(probs).cuda(), k, replace)
+        er, ec = O.sample_bias(seeds, indptr, indices, probs, k, replace, l0)
+    else:
+        row, col = dgs.ops._CAPI_cuda_sample_neighbors(dev(seeds), dev(indptr), dev(indices), k,
+                                                       replace)
+        er, ec = O.sample_uniform(seeds, indptr, indices, k, replace, l0)
+    ok = (row.dtype == idt and np.array_equal(row.cpu().numpy().astype(np.int64), er) and
+          np.array_equal(col.cpu().numpy().astype(np.int64), ec))
+    if not ok:
+        return False, cfg
+    # relabel over arbitrary int64 keys (negative and above 2^32 too), 1-3 lists of each kind
+    span = int(rng.choice([10, 1000, 1 << 20]))
+    base = int(rng.integers(-(1 << 40), 1 << 40))
+    maps = [base + rng.integers(0, span, int(rng.integers(0, 5000)))
+            for _ in range(int(rng.integers(1, 4)))]
+    reqs = [base + rng.integers(0, 2 * span, int(rng.integers(0, 5000)))
+            for _ in range(int(rng.integers(1, 4)))]
+    cfg = dict(op="relabel", span=span, base=base, maps=[m.size for m in maps],
+               reqs=[r.size for r in reqs])
+    u, rel = dgs.ops._CAPI_cuda_sampled_tensor_relabel([torch.from_numpy(m).cuda() for m in maps],
+                                                      [torch.from_numpy(r).cuda() for r in reqs])
+    eu, erel = O.relabel(maps, reqs)
+    ok = np.array_equal(u.cpu().numpy(), eu) and all(
+        np.array_equal(g.cpu().numpy(), e) for g, e in zip(rel, erel))
+    if not ok:
+        return False, cfg
+    # index_select: int32 / int64 / float32 rows of random width, int32 / int64 ids
+    vdt = [np.int32, np.int64, np.float32][int(rng.integers(3))]
+    shape = (int(rng.integers(1, 5000)),) + tuple(int(x) for x in
+                                                   rng.integers(1, 9, int(rng.integers(0, 3))))
+    data = (rng.standard_normal(shape) * 1000).astype(vdt)
+    nids = rng.integers(0, shape[0], int(rng.integers(0, 20000)))
+    cfg = dict(op="index_select", dtype=str(vdt), shape=shape, n=int(nids.size), ids=str(idt))
+    got = dgs.ops._CAPI_cuda_index_select(torch.from_numpy(data).cuda(),
+                                          torch.from_numpy(nids).to(idt).cuda())
+    return np.array_equal(got.cpu().numpy(), data[nids]), cfg
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=300)
@@ -83,6 +140,10 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--max-scale", type=int, default=14)
     ap.add_argument("--max-batch", type=int, default=2048)
+    ap.add_argument("--ops", action="store_true",
+                    help="sweep the standalone ops instead: _CAPI_cuda_sample_neighbors(_bias) "
+                         "with int32 / int64 ids, _CAPI_cuda_sampled_tensor_relabel over "
+                         "arbitrary int64 keys, _CAPI_cuda_index_select")
     ap.add_argument("--loader", action="store_true",
                     help="run 2-6 batches per configuration through PrefetchLoader (depth 1-3) "
                          "with a feature server, and check the features too")
@@ -94,7 +155,15 @@ def main():
     t0 = time.time()
     done = bad = 0
     counts = {"bias": 0, "replace": 0, "hops": [0, 0, 0]}
-    while done < a.cases and time.time() - t0 < a.seconds:
+    while a.ops and done < a.cases and time.time() - t0 < a.seconds:
+        ok, cfg = ops_case(dgs, O, rng, a.max_scale)
+        done += 1
+        if not ok:
+            bad += 1
+            print(f"MISMATCH {cfg}", flush=True)
+        if done % 20 == 0:
+            print(f"[sweep] {done} cases, {bad} mismatches, {time.time() - t0:.0f} s", flush=True)
+    while not a.ops and done < a.cases and time.time() - t0 < a.seconds:
         indptr, indices, probs, scale, ef, extra = graph(rng, a.max_scale)
         n = indptr.size - 1
         bias = bool(rng.random() < 0.4)
@@ -139,9 +208,13 @@ def main():
         if done % 20 == 0:
             print(f"[sweep] {done} cases, {bad} mismatches, {time.time() - t0:.0f} s", flush=True)
     dgs.ops._check_async_errors()
-    print(f"parity sweep: {done} cases ({counts['bias']} weighted, {counts['replace']} with "
-          f"replacement, 1/2/3 hops {counts['hops']}), {bad} mismatches, seed {a.seed}, "
-          f"{time.time() - t0:.0f} s")
+    if a.ops:
+        print(f"ops sweep: {done} cases (each: one sampling op, one relabel, one index_select), "
+              f"{bad} mismatches, seed {a.seed}, {time.time() - t0:.0f} s")
+    else:
+        print(f"parity sweep: {done} cases ({counts['bias']} weighted, {counts['replace']} with "
+              f"replacement, 1/2/3 hops {counts['hops']}), {bad} mismatches, seed {a.seed}, "
+              f"{time.time() - t0:.0f} s")
     sys.exit(1 if bad else 0)
 
 
