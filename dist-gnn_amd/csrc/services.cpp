@@ -15,19 +15,25 @@ P2PServer::P2PServer(const void *src, int64_t items, int64_t item_bytes) {
   const int64_t bytes = items * item_bytes;
   void *block = nullptr;
   DGS_HIP(hipMalloc(&block, bytes > 0 ? bytes : 1));
-  if (bytes > 0) DGS_HIP(hipMemcpy(block, src, bytes, hipMemcpyDefault));
-  item_bytes_ = item_bytes;
-  Comm &c = Comm::get();
-  rank_ = c.rank();
-  world_ = c.world();
-  ptrs_.assign(world_, nullptr);
-  ptrs_[rank_] = block;
-  items_.assign(world_, items);
-  share();
+  try {
+    if (bytes > 0) DGS_HIP(hipMemcpy(block, src, bytes, hipMemcpyDefault));
+    item_bytes_ = item_bytes;
+    Comm &c = Comm::get();
+    rank_ = c.rank();
+    world_ = c.world();
+    ptrs_.assign(world_, nullptr);
+    ptrs_[rank_] = block;
+    items_.assign(world_, items);
+    share();
+  } catch (...) {
+    // (a failed share() has opened no peer handle; every rank raises from the same point)
+    (void)hipFree(block);
+    throw;
+  }
 }
 
 P2PServer *P2PServer::adopt(void *block, int64_t items, int64_t item_bytes) {
-  P2PServer *s = new P2PServer();
+  std::unique_ptr<P2PServer> s(new P2PServer());
   s->item_bytes_ = item_bytes;
   Comm &c = Comm::get();
   s->rank_ = c.rank();
@@ -35,29 +41,71 @@ P2PServer *P2PServer::adopt(void *block, int64_t items, int64_t item_bytes) {
   s->ptrs_.assign(s->world_, nullptr);
   s->ptrs_[s->rank_] = block;
   s->items_.assign(s->world_, items);
-  s->share();
-  return s;
+  s->share();  // on failure the destructor frees the adopted block (collectively)
+  return s.release();
 }
+
+// The IPC handle exchange carries each rank's export status: a rank whose hipIpcGetMemHandle
+// fails still takes part in the all-gather, and then every rank raises naming it (instead of
+// the others waiting in the collective for a rank that has left it).
+namespace {
+struct ShareMsg {
+  hipIpcMemHandle_t h;
+  int32_t err;  // hipError_t of the export (0: ok)
+  int32_t pad;
+};
+}  // namespace
 
 void P2PServer::share() {
   Comm &c = Comm::get();
   if (world_ <= 1) return;
   items_ = c.allgather_sizes(items_[rank_]);
-  hipIpcMemHandle_t h;
-  DGS_HIP(hipIpcGetMemHandle(&h, ptrs_[rank_]));
+  ShareMsg m;
+  std::memset(&m, 0, sizeof(m));
+  m.err = (int32_t)hipIpcGetMemHandle(&m.h, ptrs_[rank_]);
+  // test hook: DGS_TEST_IPC_EXPORT_FAIL=r makes rank r report a failed export
+  static const int fail_rank = [] {
+    const char *e = std::getenv("DGS_TEST_IPC_EXPORT_FAIL");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (rank_ == fail_rank) m.err = (int32_t)hipErrorInvalidValue;
+  std::string local;
+  if (m.err != hipSuccess) {
+    (void)hipGetLastError();
+    void *base = nullptr;
+    size_t size = 0;
+    const hipError_t re = hipMemGetAddressRange(reinterpret_cast<hipDeviceptr_t *>(&base),
+                                                &size, ptrs_[rank_]);
+    (void)hipGetLastError();
+    char buf[256];
+    snprintf(buf, sizeof(buf), " (block %p of %lld items x %lld B; allocation %p, %zu B%s)",
+             ptrs_[rank_], (long long)items_[rank_], (long long)item_bytes_, base, size,
+             re == hipSuccess ? "" : ", range unknown");
+    local = buf;
+  }
   void *dh = nullptr;
-  DGS_HIP(hipMalloc(&dh, sizeof(h)));
-  DGS_HIP(hipMemcpy(dh, &h, sizeof(h), hipMemcpyHostToDevice));
+  DGS_HIP(hipMalloc(&dh, sizeof(m)));
+  DGS_HIP(hipMemcpy(dh, &m, sizeof(m), hipMemcpyHostToDevice));
   std::vector<int64_t> nbytes;
-  std::vector<void *> all = c.allgather_device(dh, sizeof(h), &nbytes);
+  std::vector<void *> all = c.allgather_device(dh, sizeof(m), &nbytes);
   DGS_HIP(hipFree(dh));
   c.barrier();
+  std::vector<ShareMsg> msgs(world_);
   for (int i = 0; i < world_; ++i) {
-    hipIpcMemHandle_t hi;
-    DGS_HIP(hipMemcpy(&hi, all[i], sizeof(hi), hipMemcpyDeviceToHost));
+    DGS_HIP(hipMemcpy(&msgs[i], all[i], sizeof(ShareMsg), hipMemcpyDeviceToHost));
     DGS_HIP(hipFree(all[i]));
+  }
+  for (int i = 0; i < world_; ++i) {
+    if (msgs[i].err == hipSuccess) continue;
+    for (int j = 0; j < world_; ++j) ptrs_[j] = j == rank_ ? ptrs_[j] : nullptr;
+    char buf[200];
+    snprintf(buf, sizeof(buf), "TensorP2PServer: rank %d could not export its block for IPC: "
+             "hipIpcGetMemHandle: %s", i, hipGetErrorString((hipError_t)msgs[i].err));
+    DGS_CHECK(false, std::string(buf) + (i == rank_ ? local : std::string()));
+  }
+  for (int i = 0; i < world_; ++i) {
     if (i == rank_) continue;
-    DGS_HIP(hipIpcOpenMemHandle(&ptrs_[i], hi, hipIpcMemLazyEnablePeerAccess));
+    DGS_HIP(hipIpcOpenMemHandle(&ptrs_[i], msgs[i].h, hipIpcMemLazyEnablePeerAccess));
   }
 }
 

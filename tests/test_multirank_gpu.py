@@ -103,3 +103,27 @@ def test_sharded_gather(results):
     assert all(res["gather_ok"] for res in results)
     # v mod 2 shard -> strided layout (peer rows through the IPC-mapped block, no table)
     assert all(res["gather_layout"] == 1 for res in results)
+
+
+def test_failed_export_raises_on_every_rank():
+    """A rank whose hipIpcGetMemHandle fails still takes part in the handle exchange, and every
+    rank raises naming it (services.cpp P2PServer::share), instead of its peers waiting in the
+    collective.  Both the TensorP2PServer constructor and an adopted service block
+    (P2PCacheFeatureServer) are checked; the process group works afterwards."""
+    world = 2
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as td:
+        procs = []
+        for r in range(world):
+            env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=str(port), LOCAL_RANK="0", DGS_TEST_IPC_EXPORT_FAIL="1")
+            procs.append(subprocess.Popen([sys.executable,
+                                           os.path.join(HERE, "ipc_fail_worker.py"),
+                                           os.path.join(td, f"r{r}.txt")], env=env))
+        rcs = [p.wait(timeout=120) for p in procs]
+        assert rcs == [0] * world, rcs
+        for r in range(world):
+            msgs = open(os.path.join(td, f"r{r}.txt")).read().splitlines()
+            assert len(msgs) == 2, msgs
+            for m in msgs:
+                assert "rank 1 could not export its block" in m, m

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--seconds", type=float, default=200.0)
     ap.add_argument("--cases", type=int, default=100000)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--full-cache", action="store_true",
+                    help="every rank caches every node (no host mirror, no peer reads)")
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -56,6 +58,8 @@ def main():
         fcache = np.nonzero((rng.integers(0, 1 << world, n) >> rank) & 1)[0]
         if fcache.size == 0:
             fcache = np.array([0])
+        if a.full_cache:
+            cache = fcache = np.arange(n)
         L = int(rng.integers(1, 4))
         fan_out = [int(rng.integers(1, 33 if bias else 41)) for _ in range(L)]
         replace = bool(rng.random() < 0.3)
