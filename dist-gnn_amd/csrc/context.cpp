@@ -92,6 +92,17 @@ std::vector<int64_t> Comm::allgather_sizes(int64_t mine) {
   return out;
 }
 
+void Comm::check_all(const std::string &err, const char *what) {
+  const std::vector<int64_t> bad = allgather_sizes(err.empty() ? 0 : 1);
+  std::string ranks;
+  for (int r = 0; r < (int)bad.size(); ++r)
+    if (bad[r]) ranks += (ranks.empty() ? "" : ", ") + std::to_string(r);
+  if (ranks.empty()) return;
+  if (bad.size() == 1) throw Error(err);
+  throw Error(std::string(what) + " failed on rank(s) " + ranks +
+              (err.empty() ? std::string(" (this rank's part succeeded)") : ": " + err));
+}
+
 void Comm::allgather_bytes(const void *send, int64_t send_bytes, void *const *recv,
                            const int64_t *recv_bytes, hipStream_t st) {
   const bool self = comm_ && self_exchange_ && !host_ag_;

@@ -60,6 +60,10 @@ class Comm {
   int world() const { return world_; }
   void barrier();
   std::vector<int64_t> allgather_sizes(int64_t mine);
+  // A setup step's local outcome made collective: `err` is this rank's error ("" = ok).  Every
+  // rank takes part; if any rank failed, every rank throws naming the failed ranks (and its own
+  // error), so no rank is left waiting in the next collective for one that has left.
+  void check_all(const std::string &err, const char *what);
   // grouped ncclSend/ncclRecv of byte payloads (recv[rank_] may alias send)
   void allgather_bytes(const void *send, int64_t send_bytes, void *const *recv,
                        const int64_t *recv_bytes, hipStream_t st);

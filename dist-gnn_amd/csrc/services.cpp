@@ -14,9 +14,15 @@ namespace dgs {
 P2PServer::P2PServer(const void *src, int64_t items, int64_t item_bytes) {
   const int64_t bytes = items * item_bytes;
   void *block = nullptr;
-  DGS_HIP(hipMalloc(&block, bytes > 0 ? bytes : 1));
+  std::string err;
   try {
+    DGS_HIP(hipMalloc(&block, bytes > 0 ? bytes : 1));
     if (bytes > 0) DGS_HIP(hipMemcpy(block, src, bytes, hipMemcpyDefault));
+  } catch (const std::exception &e) {
+    err = e.what();
+  }
+  try {
+    Comm::get().check_all(err, "TensorP2PServer: copying the block");
     item_bytes_ = item_bytes;
     Comm &c = Comm::get();
     rank_ = c.rank();
@@ -27,7 +33,7 @@ P2PServer::P2PServer(const void *src, int64_t items, int64_t item_bytes) {
     share();
   } catch (...) {
     // (a failed share() has opened no peer handle; every rank raises from the same point)
-    (void)hipFree(block);
+    if (block) (void)hipFree(block);
     throw;
   }
 }
@@ -186,34 +192,47 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
   Comm &c = Comm::get();
   rank_ = c.rank();
   world_ = c.world();
-  // sampler.cc:72.  Without a communicator every process is an independent replica (the
-  // reference would read an uninitialised rank); with the host transport ranks may share a GPU.
-  DGS_CHECK(device_id == rank_ || c.host_mode() || !c.initialized(),
-            "device_id must equal the communicator rank (sampler.cc:72)");
-  DGS_CHECK(num_nodes >= 0 && num_edges >= 0 && n_cache >= 0, "negative sizes");
-  // the biased top-k keeps row-local edge indices in 32 bits
-  if (num_edges >= INT32_MAX) {
-    int64_t prev = indptr[0];
-    for (int64_t v = 1; v <= num_nodes; ++v) {
-      DGS_CHECK(indptr[v] - prev < INT32_MAX, "a row has 2^31 - 1 or more edges");
-      prev = indptr[v];
+  hipStream_t st = nullptr;
+  // The local checks and the cache list's copy, then their outcome made collective (a rank with
+  // a bad argument must not leave its peers in the first exchange).
+  int64_t *nids = nullptr;
+  std::string err;
+  try {
+    // sampler.cc:72.  Without a communicator every process is an independent replica (the
+    // reference would read an uninitialised rank); with the host transport ranks may share a
+    // GPU.
+    DGS_CHECK(device_id == rank_ || c.host_mode() || !c.initialized(),
+              "device_id must equal the communicator rank (sampler.cc:72)");
+    DGS_CHECK(num_nodes >= 0 && num_edges >= 0 && n_cache >= 0, "negative sizes");
+    // the biased top-k keeps row-local edge indices in 32 bits
+    if (num_edges >= INT32_MAX) {
+      int64_t prev = indptr[0];
+      for (int64_t v = 1; v <= num_nodes; ++v) {
+        DGS_CHECK(indptr[v] - prev < INT32_MAX, "a row has 2^31 - 1 or more edges");
+        prev = indptr[v];
+      }
     }
+    // a cached id outside [0, num_nodes) is refused (the reference reads indptr out of bounds,
+    // utils.cu:12-42)
+    nids = device_copy_ids(cache_nids, n_cache, st);
+    DGS_CHECK(count_out_of_range(nids, n_cache, num_nodes, st) == 0,
+              "cache_nids: an id is outside [0, num_nodes)");
+  } catch (const std::exception &e) {
+    err = e.what();
+  }
+  try {
+    c.check_all(err, "P2PCacheSampler: argument checks");
+  } catch (...) {
+    if (nids) (void)hipFree(nids);
+    throw;
   }
   num_nodes_ = num_nodes;
   num_edges_ = num_edges;
   bias_ = probs != nullptr;
   if (const char *e = std::getenv("DGS_SAMPLER_MAX_CTX"))
     max_ctx_ = (size_t)std::max(1, std::atoi(e));
-  hipStream_t st = nullptr;
 
-  // this rank's cache list, shared with every rank first: it decides what the build needs.  A
-  // cached id outside [0, num_nodes) is refused (the reference reads indptr out of bounds,
-  // utils.cu:12-42).
-  int64_t *nids = device_copy_ids(cache_nids, n_cache, st);
-  if (count_out_of_range(nids, n_cache, num_nodes, st) != 0) {
-    (void)hipFree(nids);
-    DGS_CHECK(false, "cache_nids: an id is outside [0, num_nodes)");
-  }
+  // this rank's cache list, shared with every rank first: it decides what the build needs
   nids_srv_ = P2PServer::adopt(nids, n_cache, 8);
   // Rows no GPU caches are read from the host while the sampler lives (a pinned mirror of the
   // neighbour ids / probabilities); with none, the host graph only feeds the cache build (a
@@ -802,17 +821,28 @@ FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_byt
   Comm &c = Comm::get();
   rank_ = c.rank();
   world_ = c.world();
-  DGS_CHECK(device_id == rank_ || c.host_mode() || !c.initialized(),
-            "device_id must equal the communicator rank (feature_server.cc:14)");
   num_rows_ = num_rows;
   row_bytes_ = row_bytes;
   hipStream_t st = nullptr;
-  int64_t *nids = device_copy_ids(cache_nids, n_cache, st);
-  // a cached id outside [0, num_rows) is refused (the reference's hashmap would take it and
-  // its gather read out of bounds, feature_server.cc:10-61)
-  if (count_out_of_range(nids, n_cache, num_rows, st) != 0) {
-    (void)hipFree(nids);
-    DGS_CHECK(false, "cache_nids: an id is outside [0, num_rows)");
+  // the local checks, then their outcome made collective (as the sampler's)
+  int64_t *nids = nullptr;
+  std::string err;
+  try {
+    DGS_CHECK(device_id == rank_ || c.host_mode() || !c.initialized(),
+              "device_id must equal the communicator rank (feature_server.cc:14)");
+    nids = device_copy_ids(cache_nids, n_cache, st);
+    // a cached id outside [0, num_rows) is refused (the reference's hashmap would take it and
+    // its gather read out of bounds, feature_server.cc:10-61)
+    DGS_CHECK(count_out_of_range(nids, n_cache, num_rows, st) == 0,
+              "cache_nids: an id is outside [0, num_rows)");
+  } catch (const std::exception &e) {
+    err = e.what();
+  }
+  try {
+    c.check_all(err, "P2PCacheFeatureServer: argument checks");
+  } catch (...) {
+    if (nids) (void)hipFree(nids);
+    throw;
   }
   // every rank's cache list (NCCLTensorAllGather_), first: rows no GPU caches are read from the
   // host while the server lives (a pinned mirror); with none, the host matrix only fills the

@@ -1,7 +1,8 @@
-"""Worker for tests/test_multirank_gpu.py::test_failed_export_raises_on_every_rank: one rank of a
-2-rank job sharing cuda:0 whose rank 1 reports a failed IPC export (DGS_TEST_IPC_EXPORT_FAIL=1).
-Every rank must raise from the service constructor naming rank 1 -- none may wait in the
-exchange -- and the process group must still work afterwards."""
+"""Worker for tests/test_multirank_gpu.py's setup-failure tests: one rank of a 2-rank job sharing
+cuda:0.  Mode "export": rank 1 reports a failed IPC export (DGS_TEST_IPC_EXPORT_FAIL=1).  Mode
+"args": rank 1 passes an out-of-range cache id to each service.  Every rank must raise from the
+service constructor naming rank 1 -- none may wait in a setup collective -- and the process
+group must still work afterwards."""
 import os
 import sys
 
@@ -13,25 +14,34 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
-def main(out_path):
+def main(out_path, mode):
     dist.init_process_group("gloo")
+    rank = dist.get_rank()
     torch.cuda.set_device(0)
     import dgs
     dgs.ops._CAPI_set_host_comm()
-    msg = "no error"
-    try:
-        dgs.classes.TensorP2PServer(torch.arange(100, device="cuda"))
-    except RuntimeError as e:
-        msg = str(e)
+    msgs = []
     feat = torch.arange(40, dtype=torch.float32).reshape(10, 4)
-    try:
-        dgs.classes.P2PCacheFeatureServer(feat, torch.tensor([1, 2]), 0)
-    except RuntimeError as e:
-        msg += "\n" + str(e)
+    bad = torch.tensor([1, 2]) if rank == 0 else torch.tensor([1, 99])
+    if mode == "export":
+        calls = [lambda: dgs.classes.TensorP2PServer(torch.arange(100, device="cuda")),
+                 lambda: dgs.classes.P2PCacheFeatureServer(feat, torch.tensor([1, 2]), 0)]
+    else:
+        ip = torch.arange(0, 21, 2)
+        ix = torch.arange(20) % 10
+        calls = [lambda: dgs.classes.P2PCacheSampler(ip, ix, torch.Tensor(), bad, 0),
+                 lambda: dgs.classes.P2PCacheFeatureServer(feat, bad, 0)]
+    for call in calls:
+        try:
+            call()
+            msgs.append("no error")
+        except RuntimeError as e:
+            msgs.append(str(e).replace("\n", " "))
+    msg = "\n".join(msgs)
     dist.barrier()  # both ranks got here: nobody is left waiting in the exchange
     with open(out_path, "w") as f:
         f.write(msg)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2])

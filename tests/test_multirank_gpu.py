@@ -105,25 +105,39 @@ def test_sharded_gather(results):
     assert all(res["gather_layout"] == 1 for res in results)
 
 
-def test_failed_export_raises_on_every_rank():
-    """A rank whose hipIpcGetMemHandle fails still takes part in the handle exchange, and every
-    rank raises naming it (services.cpp P2PServer::share), instead of its peers waiting in the
-    collective.  Both the TensorP2PServer constructor and an adopted service block
-    (P2PCacheFeatureServer) are checked; the process group works afterwards."""
+def _setup_failure(mode, extra_env):
     world = 2
     port = _free_port()
     with tempfile.TemporaryDirectory() as td:
         procs = []
         for r in range(world):
             env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                       MASTER_PORT=str(port), LOCAL_RANK="0", DGS_TEST_IPC_EXPORT_FAIL="1")
+                       MASTER_PORT=str(port), LOCAL_RANK="0", **extra_env)
             procs.append(subprocess.Popen([sys.executable,
                                            os.path.join(HERE, "ipc_fail_worker.py"),
-                                           os.path.join(td, f"r{r}.txt")], env=env))
+                                           os.path.join(td, f"r{r}.txt"), mode], env=env))
         rcs = [p.wait(timeout=120) for p in procs]
         assert rcs == [0] * world, rcs
-        for r in range(world):
-            msgs = open(os.path.join(td, f"r{r}.txt")).read().splitlines()
-            assert len(msgs) == 2, msgs
-            for m in msgs:
-                assert "rank 1 could not export its block" in m, m
+        return [open(os.path.join(td, f"r{r}.txt")).read().splitlines() for r in range(world)]
+
+
+def test_failed_export_raises_on_every_rank():
+    """A rank whose hipIpcGetMemHandle fails still takes part in the handle exchange, and every
+    rank raises naming it (services.cpp P2PServer::share), instead of its peers waiting in the
+    collective.  Both the TensorP2PServer constructor and an adopted service block
+    (P2PCacheFeatureServer) are checked; the process group works afterwards."""
+    for msgs in _setup_failure("export", {"DGS_TEST_IPC_EXPORT_FAIL": "1"}):
+        assert len(msgs) == 2, msgs
+        for m in msgs:
+            assert "rank 1 could not export its block" in m, m
+
+
+def test_bad_argument_on_one_rank_raises_on_every_rank():
+    """One rank's out-of-range cache id (the services' first, local checks) is made collective
+    (Comm::check_all): every rank raises naming rank 1, the failing rank with its own error,
+    and no rank waits in the cache-list exchange."""
+    r0, r1 = _setup_failure("args", {})
+    for m in r0:
+        assert "failed on rank(s) 1" in m and "this rank's part succeeded" in m, m
+    for m in r1:
+        assert "failed on rank(s) 1" in m and "outside" in m, m
