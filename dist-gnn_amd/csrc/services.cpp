@@ -8,6 +8,16 @@
 
 namespace dgs {
 
+// test hook: DGS_TEST_BUILD_FAIL=r makes rank r's service build fail (after its local argument
+// checks), to test that the failure is collective
+static bool test_build_fail(int rank) {
+  static const int r = [] {
+    const char *e = std::getenv("DGS_TEST_BUILD_FAIL");
+    return e ? std::atoi(e) : -1;
+  }();
+  return rank == r;
+}
+
 // ============================================================== P2PServer
 // tensor_p2p_cache.cc:11-118: raw device block, IPC handle all-gather, peer handles opened
 // with lazy peer access; the destructor closes them behind a collective barrier.
@@ -243,28 +253,46 @@ Sampler::Sampler(const int64_t *indptr, const int64_t *indices, const float *pro
     lists[d] = (const int64_t *)nids_srv_->ptr(d);
     counts[d] = nids_srv_->items(d);
   }
-  const bool host_rows = count_uncovered(lists.data(), counts.data(), world_, num_nodes, st) > 0;
-  h_indptr_.attach(indptr, (num_nodes + 1) * 8, /*keep=*/false, st);
-  h_indices_.attach(indices, num_edges * 8, host_rows, st);
-  if (bias_) h_probs_.attach(probs, num_edges * 4, host_rows, st);
-  const int64_t *d_indptr = (const int64_t *)h_indptr_.dev;
-
-  // this rank's cached sub-CSR (sampler.cc:89-110)
+  // this rank's build (host sources, then its cached sub-CSR, sampler.cc:89-110), its outcome
+  // made collective before the sub-CSR blocks are exchanged
   int64_t *sub_indptr = nullptr;
-  DGS_HIP(hipMalloc(&sub_indptr, sizeof(int64_t) * (size_t)(n_cache + 1)));
-  extract_indptr(nids, n_cache, d_indptr, sub_indptr, st);
-  int64_t n_sub = 0;
-  DGS_HIP(hipMemcpyAsync(&n_sub, sub_indptr + n_cache, sizeof(int64_t), hipMemcpyDeviceToHost,
-                         st));
-  DGS_HIP(hipStreamSynchronize(st));
   void *sub_indices = nullptr, *sub_probs = nullptr;
-  DGS_HIP(hipMalloc(&sub_indices, sizeof(int64_t) * (size_t)(n_sub > 0 ? n_sub : 1)));
-  extract_edge_data(nids, n_cache, d_indptr, sub_indptr, h_indices_.dev, 8, sub_indices, st);
-  if (bias_) {
-    DGS_HIP(hipMalloc(&sub_probs, sizeof(float) * (size_t)(n_sub > 0 ? n_sub : 1)));
-    extract_edge_data(nids, n_cache, d_indptr, sub_indptr, h_probs_.dev, 4, sub_probs, st);
+  int64_t n_sub = 0;
+  bool host_rows = false;
+  err.clear();
+  try {
+    host_rows = count_uncovered(lists.data(), counts.data(), world_, num_nodes, st) > 0;
+    DGS_CHECK(!test_build_fail(rank_), "test hook: sampler build failure");
+    h_indptr_.attach(indptr, (num_nodes + 1) * 8, /*keep=*/false, st);
+    h_indices_.attach(indices, num_edges * 8, host_rows, st);
+    if (bias_) h_probs_.attach(probs, num_edges * 4, host_rows, st);
+    const int64_t *d_indptr = (const int64_t *)h_indptr_.dev;
+    DGS_HIP(hipMalloc(&sub_indptr, sizeof(int64_t) * (size_t)(n_cache + 1)));
+    extract_indptr(nids, n_cache, d_indptr, sub_indptr, st);
+    DGS_HIP(hipMemcpyAsync(&n_sub, sub_indptr + n_cache, sizeof(int64_t),
+                           hipMemcpyDeviceToHost, st));
+    DGS_HIP(hipStreamSynchronize(st));
+    DGS_HIP(hipMalloc(&sub_indices, sizeof(int64_t) * (size_t)(n_sub > 0 ? n_sub : 1)));
+    extract_edge_data(nids, n_cache, d_indptr, sub_indptr, h_indices_.dev, 8, sub_indices, st);
+    if (bias_) {
+      DGS_HIP(hipMalloc(&sub_probs, sizeof(float) * (size_t)(n_sub > 0 ? n_sub : 1)));
+      extract_edge_data(nids, n_cache, d_indptr, sub_indptr, h_probs_.dev, 4, sub_probs, st);
+    }
+    DGS_HIP(hipStreamSynchronize(st));
+  } catch (const std::exception &e) {
+    err = e.what();
   }
-  DGS_HIP(hipStreamSynchronize(st));
+  try {
+    c.check_all(err, "P2PCacheSampler: building the cache");
+  } catch (...) {
+    (void)hipDeviceSynchronize();
+    for (void *p : {(void *)sub_indptr, sub_indices, sub_probs})
+      if (p) (void)hipFree(p);
+    delete nids_srv_;  // (collective: every rank is on this path)
+    nids_srv_ = nullptr;
+    throw;
+  }
+  const int64_t *d_indptr = (const int64_t *)h_indptr_.dev;
   indptr_srv_ = P2PServer::adopt(sub_indptr, n_cache + 1, 8);
   indices_srv_ = P2PServer::adopt(sub_indices, n_sub, 8);
   if (bias_) probs_srv_ = P2PServer::adopt(sub_probs, n_sub, 4);
@@ -861,12 +889,30 @@ FeatureServer::FeatureServer(const void *data, int64_t num_rows, int64_t row_byt
     lp[d] = (const int64_t *)lists[d];
     counts[d] = nbytes[d] / 8;
   }
-  const bool host_rows = count_uncovered(lp.data(), counts.data(), world_, num_rows, st) > 0;
-  h_data_.attach(data, num_rows * row_bytes, host_rows, st);
+  // this rank's cache block, the outcome made collective before the blocks are exchanged
   void *block = nullptr;
-  DGS_HIP(hipMalloc(&block, (size_t)(n_cache * row_bytes > 0 ? n_cache * row_bytes : 1)));
-  gather_plain(h_data_.dev, num_rows, row_bytes, nids, 8, n_cache, block, st);
-  DGS_HIP(hipStreamSynchronize(st));
+  bool host_rows = false;
+  std::string berr;
+  try {
+    host_rows = count_uncovered(lp.data(), counts.data(), world_, num_rows, st) > 0;
+    DGS_CHECK(!test_build_fail(rank_), "test hook: feature server build failure");
+    h_data_.attach(data, num_rows * row_bytes, host_rows, st);
+    DGS_HIP(hipMalloc(&block, (size_t)(n_cache * row_bytes > 0 ? n_cache * row_bytes : 1)));
+    gather_plain(h_data_.dev, num_rows, row_bytes, nids, 8, n_cache, block, st);
+    DGS_HIP(hipStreamSynchronize(st));
+  } catch (const std::exception &e) {
+    berr = e.what();
+  }
+  try {
+    c.check_all(berr, "P2PCacheFeatureServer: building the cache");
+  } catch (...) {
+    (void)hipDeviceSynchronize();
+    if (block) (void)hipFree(block);
+    (void)hipFree(nids);
+    for (int d = 0; d < world_; ++d)
+      if (world_ > 1 && lists[d]) (void)hipFree(lists[d]);
+    throw;
+  }
   feat_srv_ = P2PServer::adopt(block, n_cache, row_bytes);
 
   ftab_.ensure(sizeof(int64_t) * (size_t)(num_rows > 0 ? num_rows : 1));

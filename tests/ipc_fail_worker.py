@@ -1,7 +1,8 @@
 """Worker for tests/test_multirank_gpu.py's setup-failure tests: one rank of a 2-rank job sharing
 cuda:0.  Mode "export": rank 1 reports a failed IPC export (DGS_TEST_IPC_EXPORT_FAIL=1).  Mode
-"args": rank 1 passes an out-of-range cache id to each service.  Every rank must raise from the
-service constructor naming rank 1 -- none may wait in a setup collective -- and the process
+"args": rank 1 passes an out-of-range cache id to each service.  Mode "build": rank 1's service
+builds fail (DGS_TEST_BUILD_FAIL=1).  Every rank must raise from the service constructor naming
+rank 1 -- none may wait in a setup collective -- and the process
 group must still work afterwards."""
 import os
 import sys
@@ -23,12 +24,15 @@ def main(out_path, mode):
     msgs = []
     feat = torch.arange(40, dtype=torch.float32).reshape(10, 4)
     bad = torch.tensor([1, 2]) if rank == 0 else torch.tensor([1, 99])
-    if mode == "export":
+    ip = torch.arange(0, 21, 2)
+    ix = torch.arange(20) % 10
+    if mode == "build":
+        calls = [lambda: dgs.classes.P2PCacheSampler(ip, ix, torch.Tensor(), torch.tensor([1]), 0),
+                 lambda: dgs.classes.P2PCacheFeatureServer(feat, torch.tensor([1, 2]), 0)]
+    elif mode == "export":
         calls = [lambda: dgs.classes.TensorP2PServer(torch.arange(100, device="cuda")),
                  lambda: dgs.classes.P2PCacheFeatureServer(feat, torch.tensor([1, 2]), 0)]
     else:
-        ip = torch.arange(0, 21, 2)
-        ix = torch.arange(20) % 10
         calls = [lambda: dgs.classes.P2PCacheSampler(ip, ix, torch.Tensor(), bad, 0),
                  lambda: dgs.classes.P2PCacheFeatureServer(feat, bad, 0)]
     for call in calls:
@@ -37,6 +41,12 @@ def main(out_path, mode):
             msgs.append("no error")
         except RuntimeError as e:
             msgs.append(str(e).replace("\n", " "))
+    if mode != "export":  # the library and the process group are usable afterwards
+        srv = dgs.classes.TensorP2PServer(torch.arange(10, device="cuda") + 100 * rank)
+        peer = srv._CAPI_get_device_tensor(1 - rank).cpu().tolist()
+        msgs.append("after: ok" if peer == [100 * (1 - rank) + i for i in range(10)]
+                    else f"after: wrong peer view {peer}")
+        del srv
     msg = "\n".join(msgs)
     dist.barrier()  # both ranks got here: nobody is left waiting in the exchange
     with open(out_path, "w") as f:

@@ -137,7 +137,21 @@ def test_bad_argument_on_one_rank_raises_on_every_rank():
     (Comm::check_all): every rank raises naming rank 1, the failing rank with its own error,
     and no rank waits in the cache-list exchange."""
     r0, r1 = _setup_failure("args", {})
-    for m in r0:
+    assert r0[-1] == r1[-1] == "after: ok", (r0, r1)
+    for m in r0[:-1]:
         assert "failed on rank(s) 1" in m and "this rank's part succeeded" in m, m
-    for m in r1:
+    for m in r1[:-1]:
         assert "failed on rank(s) 1" in m and "outside" in m, m
+
+
+def test_build_failure_on_one_rank_raises_on_every_rank():
+    """A rank whose cache build fails (host sources, sub-CSR or feature block; DGS_TEST_BUILD_FAIL
+    test hook) raises with every other rank before the blocks are exchanged, and a second
+    service can be built collectively afterwards (the process group and library state are
+    usable)."""
+    r0, r1 = _setup_failure("build", {"DGS_TEST_BUILD_FAIL": "1"})
+    assert r0[-1] == r1[-1] == "after: ok", (r0, r1)
+    for m in r0[:-1]:
+        assert "building the cache failed on rank(s) 1" in m and "succeeded" in m, m
+    for m in r1[:-1]:
+        assert "building the cache failed on rank(s) 1" in m and "test hook" in m, m
