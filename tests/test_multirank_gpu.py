@@ -155,3 +155,17 @@ def test_build_failure_on_one_rank_raises_on_every_rank():
         assert "building the cache failed on rank(s) 1" in m and "succeeded" in m, m
     for m in r1[:-1]:
         assert "building the cache failed on rank(s) 1" in m and "test hook" in m, m
+
+
+def test_random_cache_placements_match_oracle():
+    """tools/mr_sweep.py for a short while: 2 ranks, a new random graph per case whose services
+    both ranks build with a random cache placement (each node cached by no rank, one or both),
+    every rank's blocks against the oracle and its features against a host index."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(os.path.dirname(HERE), "tools", "mr_sweep.py"), "--seconds", "15",
+           "--seed", "11"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "0 mismatches" in p.stdout, p.stdout[-2000:]
