@@ -830,3 +830,17 @@ def _raw_feature_server(ptr, rows, row_bytes):
     check(lib.dgs_feature_server_create(ctypes.c_void_p(ptr), rows, row_bytes,
                                         ctypes.c_void_p(nids.data_ptr()), 1, 0, ctypes.byref(h)))
     lib.dgs_feature_server_destroy(h)
+
+
+@pytest.mark.parametrize("mode", [[], ["--loader"], ["--ops"]])
+def test_random_sweep(mode):
+    """tools/parity_sweep.py for a few seconds per mode: random graphs / caches / fan-outs through
+    the synchronous call, the loader (with features) and the standalone ops, all exact."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "tools", "parity_sweep.py"),
+                        "--seconds", "6", "--seed", "21"] + mode,
+                       capture_output=True, text=True, timeout=200)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert " 0 mismatches" in p.stdout, p.stdout[-2000:]
